@@ -13,7 +13,10 @@ checkpoint dict ``{"epoch", "model_state_dict", "optimizer_state_dict", "args", 
   decode/resize/augment on the GPU);
 * ``--resume CKPT`` (new) restores model, AdamW state, epoch, global step,
   best metric and the RNG states saved with each checkpoint (extra keys the reference ignores),
-  so a resumed run continues exactly where the saved one was. Checkpoints are read with
+  so a resumed run continues exactly where the saved one was: weights, AdamW moments, step,
+  shuffle order and the GPU noise seeds. One exception: with ``--num-workers > 0`` and
+  ``--augment``, the jitter factors are drawn in the persistent worker processes, whose RNG
+  restarts in a resumed run (same distribution, different draws). Checkpoints are read with
   ``torch.load(weights_only=True)``: everything in them is tensors and plain Python values;
 * with ``WORLD_SIZE > 1`` (torchrun) samples are sharded across ranks and gradients are summed
   over RCCL (``ddp.DataParallel``); rank 0 writes checkpoints and logs;
@@ -265,8 +268,17 @@ def main(argv=None) -> dict:
         if val_ds is not None:
             val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False)
     persistent = args.num_workers > 0
+    loader_gen = None
+    if persistent:
+        # The worker base seed is drawn once per process (when the persistent iterator is created): from
+        # its own generator, so the main-process RNG stream (shuffle order, GPU noise seeds) is the same
+        # in a resumed run as in the run it continues. The shuffle keeps the reference's source, the
+        # global RNG (a DataLoader generator would also drive the sampler).
+        loader_gen = torch.Generator().manual_seed(args.seed)
+        if sampler is None:
+            sampler = torch.utils.data.RandomSampler(train_ds)
     train_loader = DeviceLoader(train_ds, args.batch_size, shuffle=True, num_workers=args.num_workers, device=device,
-                                persistent_workers=persistent, sampler=sampler)
+                                persistent_workers=persistent, sampler=sampler, generator=loader_gen)
     val_loader = (DeviceLoader(val_ds, args.batch_size, shuffle=False, num_workers=args.num_workers, device=device,
                                persistent_workers=persistent, sampler=val_sampler) if val_ds is not None else None)
 
@@ -312,13 +324,15 @@ def main(argv=None) -> dict:
     history = []
     try:
         for epoch in range(start_epoch, args.epochs + 1):
-            if sampler is not None:
+            if hasattr(sampler, "set_epoch"):
                 sampler.set_epoch(epoch)
             t0 = time.time()
             train_metrics, global_step = run_epoch(model, train_loader, device, optimizer=optimizer,
                                                    global_step=global_step,
                                                    log_every_batches=MLFLOW_TRAIN_LOG_EVERY_BATCHES,
                                                    logger=logger, ddp=ddp)
+            if ddp is not None:  # evaluate and checkpoint with rank 0's BN running statistics on every rank
+                ddp.sync_buffers()
             val_metrics = run_epoch(model, val_loader, device, optimizer=None, ddp=ddp)[0] if val_loader else None
             metrics = _epoch_metrics(train_metrics, val_metrics, time.time() - t0)
             candidate = (val_metrics or train_metrics)["mae"]

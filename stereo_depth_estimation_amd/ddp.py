@@ -8,8 +8,11 @@ reference on the global batch:
     (train.py:334-340 on the concatenated global batch);
   * the zero-valid skip (train.py:331-332) is decided on the global count, identically on
     every rank, so parameters never diverge;
-  * BatchNorm uses per-rank batch statistics (standard DDP), running stats are
-    rank 0's when checkpointing.
+  * BatchNorm uses per-rank batch statistics (standard DDP). The running statistics
+    drift apart per rank during an epoch; ``sync_buffers()`` broadcasts rank 0's before every
+    evaluation epoch and checkpoint (torch DDP's broadcast_buffers, once per epoch instead of per
+    forward: nothing reads them between training forwards), so every rank evaluates, and
+    best.pt is chosen, with the statistics that are saved.
 Gradient buckets are contiguous slices of the flat gradient buffer (the model stores
 parameters in backward-production order), each all-reduced asynchronously on RCCL's stream
 as soon as backward finalises its last module — the collective overlaps the rest of
@@ -83,9 +86,14 @@ class DataParallel:
         self.model.engine(dev)
         flat_p, _ = self.model.flat_buffers()
         dist.broadcast(flat_p, src=0, group=self.group)
+        self.sync_buffers()
+
+    def sync_buffers(self):
+        """BatchNorm running statistics (and num_batches_tracked) from rank 0 to every rank."""
         for b in self.model.buffers():
             dist.broadcast(b, src=0, group=self.group)
-        self.model._engine.touch_state()  # eval forwards must re-pack the broadcast weights
+        if self.model._engine is not None:
+            self.model._engine.touch_state()  # eval forwards must recompute the BN coefficients / re-pack
 
     def _reducer(self):
         flat_p, flat_g = self.model.flat_buffers()

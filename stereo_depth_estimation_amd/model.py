@@ -74,6 +74,9 @@ class _UNetFunction(torch.autograd.Function):
         model._generation += 1
         ctx.model = model
         ctx.generation = model._generation
+        # an output no loss uses arrives as None in backward (not zeros): its head then gets no gradient,
+        # as in the reference, where that head is not in the autograd graph (model.py:98-104)
+        ctx.set_materialize_grads(False)
         return disp, logvar
 
     @staticmethod
@@ -90,7 +93,13 @@ class _UNetFunction(torch.autograd.Function):
         gl = None if glogvar is None else glogvar.contiguous().float()
         eng.heads(L.SD_HEADS_GRADS, gdisp=gd, glogvar=gl)
         eng.backward()
-        grads = [model._grad_views[k].clone() for k, _ in model._named_trainable()]
+        unused = set()
+        if gdisp is None:
+            unused.add("disparity_head")
+        if glogvar is None:
+            unused.add("logvar_head")
+        grads = [None if k.split(".")[0] in unused else model._grad_views[k].clone()
+                 for k, _ in model._named_trainable()]
         return (None, None, *grads)
 
 

@@ -16,10 +16,11 @@ from conftest import write_stereo_tree
 pytestmark = pytest.mark.gpu
 
 
-def _args(root, out, run, epochs, extra=()):
+def _args(root, out, run, epochs, extra=(), workers=0, augment=True):
+    aug = ["--augment", "--brightness-jitter", "0.2", "--noise-std-max", "0.02"] if augment else []
     return ["--dataset-root", str(root), "--height", "32", "--width", "48", "--epochs", str(epochs),
-            "--batch-size", "2", "--num-workers", "0", "--val-fraction", "0.25", "--output-dir", str(out),
-            "--run-name", run, "--augment", "--brightness-jitter", "0.2", "--noise-std-max", "0.02", *extra]
+            "--batch-size", "2", "--num-workers", str(workers), "--val-fraction", "0.25", "--output-dir", str(out),
+            "--run-name", run, *aug, *extra]
 
 
 def test_cli_checkpoints_and_exact_resume(tmp_path):
@@ -47,4 +48,23 @@ def test_cli_checkpoints_and_exact_resume(tmp_path):
     for pid, st in a["optimizer_state_dict"]["state"].items():
         for k, v in st.items():
             assert torch.equal(torch.as_tensor(v), torch.as_tensor(b["optimizer_state_dict"]["state"][pid][k])), (pid, k)
+    assert a["metrics"]["train_mae"] == b["metrics"]["train_mae"]
+
+
+def test_cli_exact_resume_with_persistent_workers(tmp_path):
+    """--num-workers 2 (persistent workers, the reference's loader setup): the worker base seed comes
+    from its own generator, so the shuffle order and everything downstream continue exactly after
+    --resume (augmentation off: its jitter is drawn inside the workers, see cli.py)."""
+    from stereo_depth_estimation_amd import cli
+
+    write_stereo_tree(tmp_path / "data", scenes=2, frames=4, hw=(40, 52), seed=9)
+    kw = dict(workers=2, augment=False)
+    cli.main(_args(tmp_path / "data", tmp_path / "out", "straight", 3, **kw))
+    cli.main(_args(tmp_path / "data", tmp_path / "out", "resumed", 2, **kw))
+    part = tmp_path / "out" / "resumed" / "checkpoints" / "last.pt"
+    cli.main(_args(tmp_path / "data", tmp_path / "out", "resumed", 3, ["--resume", str(part)], **kw))
+    a = torch.load(tmp_path / "out" / "straight" / "checkpoints" / "last.pt", map_location="cpu", weights_only=True)
+    b = torch.load(part, map_location="cpu", weights_only=True)
+    for k, v in a["model_state_dict"].items():
+        assert torch.equal(v, b["model_state_dict"][k]), k
     assert a["metrics"]["train_mae"] == b["metrics"]["train_mae"]

@@ -1,5 +1,7 @@
-"""Data-parallel train step end to end on the GPU: two ranks (`gloo` over device tensors, both on
-cuda:0 — the single-GPU box has one card; the 8-GPU RCCL run is the driver's bench).
+"""Data-parallel train step end to end on the GPU: two ranks, either `gloo` over device tensors with
+both ranks on cuda:0 (the single-GPU box has one card), or the production path — RCCL (`nccl`
+backend) with one rank per GPU and the async bucket all-reduces on RCCL's stream overlapping
+backward — when the box has two or more GPUs (skipped otherwise).
 
 * Both ranks train on the SAME batch: per-rank BN statistics then equal the single-process ones,
   the global valid count is 2x, and the SUM of the two gradients normalised by it equals the
@@ -7,6 +9,8 @@ cuda:0 — the single-GPU box has one card; the 8-GPU RCCL run is the driver's b
   single-process steps (fp32 path; only reduction order differs).
 * Rank 0 gets a batch with no valid pixel, rank 1 a normal one: the skip of train.py:331-332 is
   decided on the global count, so both ranks step and stay bit-identical.
+* Different batches per rank: the per-rank BN running statistics differ after a step and are equal
+  again after ``DataParallel.sync_buffers()`` (called by the CLI before evaluation / checkpoints).
 """
 
 from __future__ import annotations
@@ -28,7 +32,7 @@ def _free_port() -> int:
     return port
 
 
-def _worker(rank: int, world: int, port: int, q):
+def _worker(rank: int, world: int, port: int, q, backend: str = "gloo"):
     import torch.distributed as dist
 
     from stereo_depth_estimation_amd.data import synthetic_batch
@@ -37,10 +41,14 @@ def _worker(rank: int, world: int, port: int, q):
     from stereo_depth_estimation_amd.optim import FusedAdamW
     from stereo_depth_estimation_amd.train import train_step
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dev = torch.device("cuda", rank if backend == "nccl" else 0)
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        dev = torch.device("cuda:0")
 
         def make():
             torch.manual_seed(0)
@@ -71,7 +79,20 @@ def _worker(rank: int, world: int, port: int, q):
         gathered = [torch.empty_like(p1) for _ in range(world)]
         dist.all_gather(gathered, p1)
         in_sync = all(torch.equal(gathered[0], g) for g in gathered)
-        q.put((rank, diff, moved, in_sync, None))
+        # 3) different batches per rank: BN running statistics drift apart until sync_buffers()
+        m3, o3 = make()
+        dp3 = DataParallel(m3)
+        b3 = synthetic_batch(2, 32, 48, seed=11 + rank, device=dev)
+        dp3.step(m3, o3, b3["input"], b3["target"], b3["valid_mask"])
+        bufs = torch.cat([t.detach().double().flatten() for t in m3.buffers()])
+        gathered = [torch.empty_like(bufs) for _ in range(world)]
+        dist.all_gather(gathered, bufs)
+        drifted = not all(torch.equal(gathered[0], g) for g in gathered)
+        dp3.sync_buffers()
+        bufs = torch.cat([t.detach().double().flatten() for t in m3.buffers()])
+        dist.all_gather(gathered, bufs)
+        synced = all(torch.equal(gathered[0], g) for g in gathered)
+        q.put((rank, diff, moved, in_sync and drifted and synced, None))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, None, None, None, repr(e)))
         raise
@@ -79,14 +100,17 @@ def _worker(rank: int, world: int, port: int, q):
         dist.destroy_process_group()
 
 
-def test_ddp_two_ranks_match_single_process_and_skip_globally():
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_ddp_two_ranks_match_single_process_and_skip_globally(backend):
     import torch.multiprocessing as mp
 
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL two-rank test needs two GPUs (one rank per device)")
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, backend)) for r in range(world)]
     for p in procs:
         p.start()
     results = sorted(q.get(timeout=300) for _ in range(world))
@@ -96,5 +120,5 @@ def test_ddp_two_ranks_match_single_process_and_skip_globally():
         assert err is None, f"rank {rank}: {err}"
         assert diff <= 1e-6, f"rank {rank}: DDP params differ from single-process by {diff}"
         assert moved, f"rank {rank}: zero-local-valid rank skipped the step (skip must use the global count)"
-        assert in_sync, f"rank {rank}: ranks diverged"
+        assert in_sync, f"rank {rank}: ranks diverged, or BN buffers not re-synced by sync_buffers()"
     assert all(p.exitcode == 0 for p in procs)
