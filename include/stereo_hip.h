@@ -64,6 +64,9 @@ typedef struct sd_src {
 } sd_src;
 
 int sd_version(void);
+/* Diagnostics: device buffer for the per-wave cycle counters of timing builds (-DWG_EXP=1024; no effect
+   otherwise). Not a reference interface. */
+int sd_debug_buffer(void* dev_ptr);
 const char* sd_last_error(void);
 int sd_device_init(int device);
 

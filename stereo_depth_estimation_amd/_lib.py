@@ -88,6 +88,7 @@ _PJOB = ctypes.POINTER(SdPackJob)
 # name -> (restype, argtypes); mirrors include/stereo_hip.h
 PROTOTYPES: dict[str, tuple] = {
     "sd_version": (_i, []),
+    "sd_debug_buffer": (_i, [_p]),
     "sd_last_error": (ctypes.c_char_p, []),
     "sd_device_init": (_i, [_i]),
     "sd_pack_input": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _p]),

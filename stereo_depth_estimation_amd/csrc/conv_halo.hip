@@ -18,6 +18,11 @@
 namespace {
 
 constexpr int CK = 32;                           // channels per chunk
+#ifndef WG_EXP
+#define WG_EXP 0  // timing experiments only. wgrad<64>: bit 0 no MFMA phase, 1 no tile loads after the first,
+                  // 2 no LDS stores; halo conv: bit 3 no MFMA phase, 4 no halo loads after the first item, 5 no halo LDS
+                  // stores; k_halo_wgrad_ws: bit 6 no MFMA phase, 7 no LDS stores, 8 no loads and no stores
+#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 struct HaloSrc {
@@ -104,6 +109,33 @@ __device__ __forceinline__ uint4 halo_finish(const HaloCol& hc, bool ok, uint4 r
                 (__bf16)fmaxf(__builtin_fmaf(__uint_as_float(w[i] & 0xffff0000u), s[2 * i + 1], h[2 * i + 1]), 0.f);
         }
         v = *reinterpret_cast<uint4*>(&o);
+    }
+    return ok ? v : make_uint4(0, 0, 0, 0);
+}
+
+// halo_finish with the ReLU taken on the rounded bf16 pair (v_pk_max_i16 against 0: a bf16 is <= 0 exactly
+// when its sign bit is set or it is zero, and rounding preserves the sign), one instruction per pair
+// instead of two v_max_f32. Same values as halo_finish for every finite input.
+typedef short short2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 halo_finish_pk(const HaloCol& hc, bool ok, uint4 raw) {
+    uint4 v = raw;
+    if (hc.bn) {
+        const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
+        const float s[8] = {hc.s0.x, hc.s0.y, hc.s0.z, hc.s0.w, hc.s1.x, hc.s1.y, hc.s1.z, hc.s1.w};
+        const float h[8] = {hc.h0.x, hc.h0.y, hc.h0.z, hc.h0.w, hc.h1.x, hc.h1.y, hc.h1.z, hc.h1.w};
+        bf16x8 pr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            pr[2 * i] = (__bf16)__builtin_fmaf(__uint_as_float(w[i] << 16), s[2 * i], h[2 * i]);
+            pr[2 * i + 1] = (__bf16)__builtin_fmaf(__uint_as_float(w[i] & 0xffff0000u), s[2 * i + 1], h[2 * i + 1]);
+        }
+        const uint4 u = __builtin_bit_cast(uint4, pr);
+        const unsigned ui[4] = {u.x, u.y, u.z, u.w};
+        unsigned o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            o[i] = __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(short2_t, ui[i]), short2_t{0, 0}));
+        v = make_uint4(o[0], o[1], o[2], o[3]);
     }
     return ok ? v : make_uint4(0, 0, 0, 0);
 }
@@ -299,7 +331,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             for (int i = 0; i < HP; ++i) {
                 const bool ok = hin[i] & q.hc.cok;
                 m |= (unsigned)ok << i;
-                q.hr[i] = *reinterpret_cast<const uint4*>(q.hc.base + (ok ? (size_t)hpix[i] * q.hc.C + q.hc.c : 0));
+                if (!(WG_EXP & 16) || ld_item == 0)
+                    q.hr[i] = *reinterpret_cast<const uint4*>(q.hc.base + (ok ? (size_t)hpix[i] * q.hc.C + q.hc.c : 0));
             }
             q.m = m;
             if (++ld_cc == nchunks) {
@@ -310,6 +343,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         };
         auto store = [&](auto S, int buf) __attribute__((always_inline)) {  // halo set S and the weights in wr -> LDS buffer buf
             __bf16* hx = smem + buf * BUF;
+            if (!(WG_EXP & 32))
 #pragma unroll
             for (int i = 0; i < HP; ++i) {  // every piece lands inside the halo region
                 const int item = ltid + i * 256;
@@ -425,6 +459,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             for (int i = 0; i < RT; ++i)
                 af[slot_][i] = *reinterpret_cast<const bf16x8*>(hx + (abase[i] + toff) * HX_LD + c8 * 8);
         };
+        if (!(WG_EXP & 8)) {
 #pragma unroll
         for (int step = 0; step < PF; ++step) read_frags(step);
 #pragma unroll
@@ -438,6 +473,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 for (int t = 0; t < NT; ++t)
                     acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[sl][t], af[sl][i], acc[i][t], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
+        }
         }
 
         if (++cc == nchunks) {
@@ -572,6 +608,7 @@ struct HWgArgs {
     int M, N;          // N = 9 * ctot
     float* slab;
     int xcd;           // 1: XCD-contiguous block numbering (block count % 8 == 0)
+    unsigned long long* dbg;  // timing-diagnostic builds only (WG_EXP & 1024): per-wave cycle counters
 };
 
 constexpr int XW_LD = CK + 16;  // halo pixel stride for transposed reads (96 B)
@@ -764,10 +801,10 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
         // M % 64: one tile in flight (a second register set would halve the waves per SIMD)
         if (t_begin < t_end) load_tile(S0, t_begin);
         for (int tile = t_begin; tile < t_end; ++tile) {
-            store_tile(S0);
+            if (!(WG_EXP & 4)) store_tile(S0);
             __syncthreads();
-            if (tile + 1 < t_end) load_tile(S0, tile + 1);
-            compute();
+            if (!(WG_EXP & 2) && tile + 1 < t_end) load_tile(S0, tile + 1);
+            if (!(WG_EXP & 1)) compute();
             __syncthreads();
         }
     }
@@ -786,6 +823,301 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
                     slab[(size_t)co * p.N + tap * p.x.ctot + ci] = acc[tap][i][r];
                 }
     }
+}
+
+
+// =====================================================================================
+// wgrad, warp-specialised: M % 64 == 0 and x channels % 64 == 0 (every M % 64 layer but enc2.0)
+// =====================================================================================
+// One 512-thread block per CU. A block owns 64 dy channels (rows of dW) x 64 x channels x 9 taps
+// and a range of 128-pixel tiles (split-K). Waves 4-7 stage tile t+1 (the dy rows, and the x halo
+// through BN+ReLU) into one LDS buffer while waves 0-3 run tile t's MFMAs from the other, one
+// barrier per tile: the one-role-per-wave layout of k_halo_conv. (k_halo_wgrad interleaves both
+// roles in every wave at 2 blocks per CU; timing runs with either role removed measured its MFMA
+// phase alone at 74 us of 136 us for 120x160x64x64: the staging was not hidden.)
+// MFMA wave w owns all 64 dy channels (4 16-row tiles) x the 16 x channels 16w..16w+15 x 9 taps:
+// 36 accumulators of v_mfma_f32_16x16x32_bf16 (144 registers). Per 32-pixel k-step it reads 4 dy
+// and 9 x-halo fragments (ds_read_b64_tr_b16 pairs) for 36 MFMAs (26 reads per 36 MFMAs; the
+// 2-block kernel reads 22 per 18). The 4 k-steps x 9 taps of a tile run as one straight-line
+// stream of tap-steps with the fragment reads WS_PD tap-steps ahead in a register ring.
+// The halo is laid out with a fixed row pitch of WS_HP pixels (tiles with tw <= 32, th <= 6), so the 9
+// tap offsets of a fragment read are compile-time immediates: no address arithmetic per tap-step (a
+// runtime pitch cost 4 VALU per 4 MFMAs, half the issue slots the 16x16x32 MFMAs leave free).
+constexpr int WS_TPX = 128;                     // pixels per tile (4 k-steps)
+constexpr int WS_HP = 34, WS_HR = 8;            // halo row pitch (pixels) and rows (th + 2 <= 8, tw + 2 <= 34)
+constexpr int WS_HMAX = 288;                    // halo pixel slots staged (>= WS_HR * WS_HP, 9 pieces per thread)
+constexpr int WS_CI = 64;                       // x channels per block
+constexpr int WS_LD = 64 + 16;                  // 160-B rows (dy and halo): conflict-free transposed reads
+constexpr int WS_PD = 5;                        // tap-steps of fragment read-ahead (4 MFMAs each)
+
+__global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
+    constexpr int KS = WS_TPX / 32;
+    constexpr int DY_E = WS_TPX * WS_LD, BUF = DY_E + WS_HMAX * WS_LD;  // elements per LDS buffer
+    constexpr int DYP = WS_TPX * 8 / 256, HXP = WS_HMAX * 8 / 256;     // 16-B pieces per loader thread
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool is_loader = tid >= 256;
+    const int wid = (tid >> 6) & 3;
+    int cc = blockIdx.x, zb = blockIdx.z, split = blockIdx.y;
+    if (p.xcd) {  // XCD-contiguous numbering, as in k_halo_wgrad
+        const int G = gridDim.x * gridDim.y * gridDim.z;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int lg = (L & 7) * (G >> 3) + (L >> 3);
+        cc = lg % gridDim.x;
+        const int r = lg / gridDim.x;
+        zb = r % gridDim.z;
+        split = r / gridDim.z;
+    }
+    const int mb = zb * 64;
+    const int t_begin = split * p.tiles_per_split;
+    const int ntile = max(0, min(p.ntiles, t_begin + p.tiles_per_split) - t_begin);
+    const int mvalid = p.th * p.tw;
+
+    if (is_loader) {
+        // =========================================================== loader waves
+        // item = ltid + 256 i -> (pixel item >> 3, 16-B piece ltid & 7): the piece (8 channels) is fixed per
+        // thread, and an 8-lane ds_write_b128 group covers one pixel's 8 pieces at the 10-slot row
+        // stride: conflict-free
+        const int ltid = tid - 256, piece = ltid & 7, pix0 = ltid >> 3;
+        unsigned dyrc[(DYP + 1) / 2], hgeo[(HXP + 1) / 2];  // (row << 8 | col), 0xffff past the tile / halo
+#pragma unroll
+        for (int i = 0; i < DYP; i += 2) {
+            unsigned e[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int m = pix0 + 32 * (i + h);
+                const int hm = m / p.tw;
+                e[h] = (i + h < DYP && m < mvalid) ? (unsigned)(hm << 8 | (m - hm * p.tw)) : 0xffffu;
+            }
+            dyrc[i / 2] = e[0] | e[1] << 16;
+        }
+#pragma unroll
+        for (int i = 0; i < HXP; i += 2) {
+            unsigned e[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int px = pix0 + 32 * (i + h);
+                const int hy = px / WS_HP, hx = px - hy * WS_HP;
+                e[h] = (i + h < HXP && hy < p.th + 2 && hx < p.hw) ? (unsigned)(hy << 8 | hx) : 0xffffu;
+            }
+            hgeo[i / 2] = e[0] | e[1] << 16;
+        }
+        // the block's 64 x channels come from one source (the dispatcher requires chans[0] % 64 == 0)
+        const bool src1 = cc * WS_CI >= p.x.c0;
+        const __bf16* xsrc = src1 ? p.x.p1 : p.x.p0;
+        const int xC = src1 ? p.x.c1 : p.x.c0;
+        const HaloCol hc = halo_col(p.x, cc * WS_CI + piece * 8, p.dy);  // this thread's 8 channels (BN affine)
+        // Per-piece element offsets from the tile origin (h0, w0), fixed for the launch: a piece's buffer
+        // offset is then one add, its bounds test four compares against per-tile scalars, and a piece
+        // outside the image / tile gets an offset past the buffer's range, which the buffer load returns
+        // as zeros without touching memory (loads of a fixed dummy address made every CU hit one line)
+        int dpo[DYP], xpo[HXP];
+#pragma unroll
+        for (int i = 0; i < DYP; ++i) {
+            const unsigned rc = (dyrc[i / 2] >> (16 * (i & 1))) & 0xffffu;
+            dpo[i] = ((int)(rc >> 8) * p.W + (int)(rc & 0xff)) * p.M + mb + piece * 8;
+        }
+#pragma unroll
+        for (int i = 0; i < HXP; ++i) {
+            const unsigned gg = (hgeo[i / 2] >> (16 * (i & 1))) & 0xffffu;
+            xpo[i] = (((int)(gg >> 8) - 1) * p.W + (int)(gg & 0xff) - 1) * xC + hc.c;
+        }
+        struct TSet {
+            uint4 d[DYP], x[HXP];
+            unsigned xm;
+        };
+        TSet sa, sb;
+        auto load = [&](TSet& q, int tile) __attribute__((always_inline)) {
+            if (WG_EXP & 256) return;
+            const int tx = tile % p.tiles_x;
+            const int rest = tile / p.tiles_x;
+            const int ty = rest % p.tiles_y, b = rest / p.tiles_y;
+            const int h0 = ty * p.th, w0 = tx * p.tw;
+            const size_t img = (size_t)b * p.H * p.W;
+            const int tpx = h0 * p.W + w0;
+            const int nimg = p.H * p.W;
+            const __amdgpu_buffer_rsrc_t rdy =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + img * p.M), (short)0, nimg * p.M * 2, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rx =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(xsrc + img * xC), (short)0, nimg * xC * 2, 0x00020000);
+            // halo piece (hy, hx) is inside the image iff 1 - h0 <= hy < H - h0 + 1 and 1 - w0 <= hx < W - w0 + 1
+            int rlo = 1 - h0, rhi = p.H - h0 + 1, clo = 1 - w0, chi = p.W - w0 + 1;
+            if (tile >= t_begin + ntile) rhi = rlo;  // past the block's range: every piece out of range, no traffic
+            const int dbase = tpx * p.M, xbase = tpx * xC;
+            unsigned xm = 0;
+#pragma unroll
+            for (int i = 0; i < DYP; ++i) {
+                const unsigned rc = (dyrc[i / 2] >> (16 * (i & 1))) & 0xffffu;
+                const bool ok = (rc != 0xffffu) & ((int)(rc >> 8) < rhi - 1) & ((int)(rc & 0xff) < chi - 1) & (rhi > rlo);
+                const unsigned off = ok ? (unsigned)(dbase + dpo[i]) * 2u : 0x80000000u;
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rdy, off, 0, 0);
+                q.d[i] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+#pragma unroll
+            for (int i = 0; i < HXP; ++i) {
+                const unsigned gg = (hgeo[i / 2] >> (16 * (i & 1))) & 0xffffu;
+                const int hy = (int)(gg >> 8), hx = (int)(gg & 0xff);
+                const bool ok = (gg != 0xffffu) & (hy >= rlo) & (hy < rhi) & (hx >= clo) & (hx < chi);
+                xm |= (unsigned)ok << i;
+                const unsigned off = ok ? (unsigned)(xbase + xpo[i]) * 2u : 0x80000000u;
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+                q.x[i] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+            q.xm = xm;
+        };
+        auto store = [&](TSet& q, int buf) __attribute__((always_inline)) {
+            if (WG_EXP & (128 | 256)) return;
+            __bf16* dys = smem + buf * BUF;
+            __bf16* hxs = dys + DY_E;
+#pragma unroll
+            for (int i = 0; i < DYP; ++i)  // out-of-range pieces were loaded as zeros
+                *reinterpret_cast<uint4*>(dys + (pix0 + 32 * i) * WS_LD + piece * 8) = q.d[i];
+#pragma unroll
+            for (int i = 0; i < HXP; ++i)
+                *reinterpret_cast<uint4*>(hxs + (pix0 + 32 * i) * WS_LD + piece * 8) =
+                    halo_finish_pk(hc, (q.xm >> i) & 1u, q.x[i]);
+        };
+        // tile i is in set i & 1 from its load until its store, which happens one tile ahead of the MFMA
+        // waves; each set is refilled right after its store, so two tiles' loads are in flight. Loads are
+        // unconditional (past the range they fetch nothing): with a conditional younger load the compiler
+        // cannot count vmcnt and drains every load before each store
+        constexpr bool DG = (WG_EXP & 1024) != 0;
+        unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t1 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
+#define WS_T0() if (DG) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); t0 = __builtin_amdgcn_s_memtime(); }
+#define WS_T1(acc_) if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); acc_ += t1 - t0; }
+        load(sa, t_begin);
+        load(sb, t_begin + 1);
+        if (ntile > 0) store(sa, 0);
+        load(sa, t_begin + 2);
+        __syncthreads();
+        for (int i = 0; i < ntile; i += 2) {
+            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            if (i + 1 < ntile) store(sb, 1);
+            WS_T1(t_st)
+            load(sb, t_begin + i + 3);
+            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; }
+            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            __syncthreads();
+            if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+            if (i + 1 >= ntile) break;
+            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            if (i + 2 < ntile) store(sa, 0);
+            WS_T1(t_st)
+            load(sa, t_begin + i + 4);
+            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; }
+            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            __syncthreads();
+            if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+        }
+        if (DG && p.dbg && lane == 0) {
+            unsigned long long* d = p.dbg + ((size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + 4 + wid) * 4;
+            d[0] = t_st;
+            d[1] = t_ld;
+            d[2] = t_br;
+            d[3] = __builtin_amdgcn_s_memtime() - t_all;
+        }
+#undef WS_T0
+#undef WS_T1
+        return;
+    }
+
+    // =============================================================== MFMA waves
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int pc = 16 * (g >> 1) + 4 * (g & 1) + q;  // pixel within the k-step (0..23), +8 for the 2nd read
+    const int ci0 = 16 * wid;
+    // byte offsets (within the halo region) of this lane's two halo rows of each k-step at tap (0,0)
+    unsigned xoff[KS][2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int m = ks * 32 + pc + 8 * h;
+            const int hm = m / p.tw;
+            const int px = m < mvalid ? hm * WS_HP + (m - hm * p.tw) : 0;  // dy is 0 past the tile
+            xoff[ks][h] = (unsigned)(px * WS_LD + ci0 + 4 * pp) * 2u;
+        }
+    f32x4 acc[9][4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int NSTEP = KS * 9;
+    bf16x8 bring[WS_PD + 1];
+    bf16x8 aring[2][4];
+    const char* lds = reinterpret_cast<const char*>(smem);
+    constexpr bool DG = (WG_EXP & 1024) != 0;
+    unsigned long long t_cp = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
+    __syncthreads();
+    for (int it = 0; it < ntile; ++it) {
+        if (DG) t0 = __builtin_amdgcn_s_memtime();
+        const unsigned bufb = (unsigned)((it & 1) * BUF * 2);                           // byte offset of this buffer
+        unsigned abase = bufb + (unsigned)(pc * WS_LD + 4 * pp) * 2u;
+        asm volatile("" : "+v"(abase));
+        unsigned xb[KS][2];  // this tile's read addresses; opaque so the compiler keeps them per tile
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                xb[ks][h] = xoff[ks][h] + bufb + (unsigned)(DY_E * 2);
+                asm volatile("" : "+v"(xb[ks][h]));
+            }
+        auto issue = [&](int j) __attribute__((always_inline)) {
+            const int ks = j / 9, tap = j - ks * 9;
+            if (tap == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const __bf16* a0 = reinterpret_cast<const __bf16*>(lds + abase) + ks * 32 * WS_LD + i * 16;
+                    aring[ks & 1][i] = tr_pair(a0, a0 + 8 * WS_LD);
+                }
+            }
+            const int toff = ((tap / 3) * WS_HP + tap % 3) * WS_LD;  // compile-time: folds into the ds offset
+            bring[j % (WS_PD + 1)] = tr_pair(reinterpret_cast<const __bf16*>(lds + xb[ks][0]) + toff,
+                                             reinterpret_cast<const __bf16*>(lds + xb[ks][1]) + toff);
+        };
+        if (!(WG_EXP & 64)) {
+#pragma unroll
+        for (int j = 0; j < WS_PD; ++j) issue(j);
+#pragma unroll
+        for (int j = 0; j < NSTEP; ++j) {
+            if (j + WS_PD < NSTEP) issue(j + WS_PD);
+            __builtin_amdgcn_sched_barrier(0);
+            const int ks = j / 9, tap = j - ks * 9;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aring[ks & 1][i], bring[j % (WS_PD + 1)], acc[tap][i],
+                                                                     0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        }
+        if (DG) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_cp += t1 - t0;
+            t0 = t1;
+        }
+        __syncthreads();
+        if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+    }
+    if (DG && p.dbg && lane == 0) {
+        unsigned long long* d = p.dbg + ((size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + wid) * 4;
+        d[0] = t_cp;
+        d[1] = 0;
+        d[2] = t_br;
+        d[3] = __builtin_amdgcn_s_memtime() - t_all;
+    }
+    // slab[split][co][tap*ctot + cc*64 + ci]   (C layout 16x16: row = 4*(lane>>4) + r, col = lane&15)
+    float* slab = p.slab + (size_t)split * p.M * p.N;
+    const int ci = cc * WS_CI + ci0 + (lane & 15);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = mb + i * 16 + 4 * (lane >> 4) + r;
+                slab[(size_t)co * p.N + tap * p.x.ctot + ci] = acc[tap][i][r];
+            }
 }
 
 }  // namespace
@@ -990,24 +1322,66 @@ static HTile wgrad_tile(int H, int W) {
     return best;
 }
 
+// diagnostics: per-wave cycle counters of timing builds (WG_EXP & 1024) go to this device buffer
+static unsigned long long* g_wg_dbg = nullptr;
+extern "C" int sd_debug_buffer(void* p) {
+    g_wg_dbg = (unsigned long long*)p;
+    return 0;
+}
+
+// warp-specialised wgrad (k_halo_wgrad_ws) for M % 64 == 0 with x channels % 64 == 0; SD_WG_WS=0 keeps
+// k_halo_wgrad (A/B runs)
+static bool wgrad_ws(int M, int N) {
+    static const bool on = [] {
+        const char* e = getenv("SD_WG_WS");
+        return !(e && atoi(e) == 0);
+    }();
+    return on && M % 64 == 0 && N % 9 == 0 && (N / 9) % WS_CI == 0;
+}
+
+// its tile: th x tw <= 128 pixels, tw <= 32 and th <= 6 (the fixed-pitch halo), minimising the MFMA work
+// (a tile always costs 128 pixels) plus the halo staging over the image
+static HTile wgrad_tile_ws(int H, int W) {
+    HTile best{4, 32, 4};
+    double best_cost = 1e300;
+    for (int tw = W < 8 ? W : 8; tw <= (W < WS_HP - 2 ? W : WS_HP - 2); ++tw) {
+        if (tw != W && tw != 32 && W % tw) continue;
+        for (int th = 1; th <= H && th * tw <= WS_TPX; ++th) {
+            if (th + 2 > WS_HR) break;
+            const double tiles = (double)cdiv(H, th) * cdiv(W, tw);
+            const double cost = tiles * (WS_TPX + 0.5 * (th + 2) * (tw + 2));
+            if (cost < best_cost) {
+                best_cost = cost;
+                best = {th, tw, 4};
+            }
+        }
+    }
+    return best;
+}
+
 int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
-    const HTile t = wgrad_tile(H, W);
-    const int nblk = cdiv(N / 9, CK) * (M == 32 ? 1 : M / 64);
+    const bool ws = wgrad_ws(M, N);
+    const HTile t = ws ? wgrad_tile_ws(H, W) : wgrad_tile(H, W);
+    const int nblk = ws ? (N / 9 / WS_CI) * (M / 64) : cdiv(N / 9, CK) * (M == 32 ? 1 : M / 64);
     const int nt = cdiv(W, t.tw) * cdiv(H, t.th) * batch;
     static const int blocks = [] {  // SD_WG_BLOCKS: total split-K blocks (A/B runs)
         const char* e = getenv("SD_WG_BLOCKS");
         return e && atoi(e) > 0 ? atoi(e) : 512;
     }();
-    int splits = cdiv(blocks, nblk);  // one round of blocks at 2 per CU (LDS); half the slab of 1024
+    // one round of blocks: 2 per CU for k_halo_wgrad (LDS, registers), 1 per CU for the warp-specialised one
+    int splits = cdiv(ws ? PERSIST_BLOCKS : blocks, nblk);
     if (splits > nt) splits = nt;
     return splits < 1 ? 1 : splits;
 }
 
-const char* sd_halo_wgrad_name(int M) { return M == 32 ? "k_halo_wgrad<32>" : "k_halo_wgrad<64>"; }
+const char* sd_halo_wgrad_name(int M, int N, int c0) {
+    return M == 32 ? "k_halo_wgrad<32>" : wgrad_ws(M, N) && c0 % WS_CI == 0 ? "k_halo_wgrad_ws" : "k_halo_wgrad<64>";
+}
 
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
                   hipStream_t st) {
-    const HTile t = wgrad_tile(H, W);
+    const bool ws = wgrad_ws(M, N) && b.chans[0] % WS_CI == 0;  // one source per 64-channel block
+    const HTile t = ws ? wgrad_tile_ws(H, W) : wgrad_tile(H, W);
     HWgArgs p;
     p.dy = (const __bf16*)a.ptr[0];
     p.x = make_halo_src(b);
@@ -1024,6 +1398,15 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
     p.M = M;
     p.N = N;
     p.slab = slab;
+    p.dbg = g_wg_dbg;
+    if (ws) {
+        const int ncc = p.x.ctot / WS_CI;
+        p.xcd = halo_xcd_enabled() && (ncc * splits * (M / 64)) % 8 == 0;
+        SD_REQUIRE(t.th + 2 <= WS_HR && t.tw + 2 <= WS_HP && t.th * t.tw <= WS_TPX, "sd_wgrad_gemm(halo ws): tile %dx%d",
+                   t.th, t.tw);
+        hipLaunchKernelGGL(k_halo_wgrad_ws, dim3(ncc, splits, M / 64), dim3(512), 0, st, p);
+        return sd_check_launch("sd_wgrad_gemm(halo ws)");
+    }
     p.xcd = halo_xcd_enabled() && (cdiv(p.x.ctot, CK) * splits * (M == 32 ? 1 : M / 64)) % 8 == 0;
     SD_REQUIRE(p.nhalo <= HMAX && t.th * t.tw <= WG_MAXPX, "sd_wgrad_gemm(halo): tile %dx%d", t.th, t.tw);
     if (M == 32) {

@@ -156,7 +156,11 @@ def test_conv3x3_dual_source_and_dgrad_split(prec, B, H, W, c0, c1, co):
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 10, 14, 24, 32),
                                          # bf16 halo wgrad: 64-row dy blocks, flattened tiles of any shape
                                          (2, 15, 20, 64, 64), (1, 30, 40, 40, 128), (1, 13, 50, 16, 192),
-                                         (1, 9, 300, 8, 64)])
+                                         (1, 9, 300, 8, 64),
+                                         # warp-specialised wgrad (M % 64, x channels % 64): 2 x-channel blocks,
+                                         # 2 dy blocks, ragged tiles, many tiles per split
+                                         (2, 30, 40, 128, 64), (1, 13, 50, 64, 128), (3, 17, 33, 64, 64),
+                                         (1, 120, 160, 64, 64)])
 def test_conv3x3_wgrad(prec, B, H, W, ci, co):
     lib = L()
     torch.manual_seed(2)
@@ -174,6 +178,30 @@ def test_conv3x3_wgrad(prec, B, H, W, ci, co):
     lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(), lib.stream_handle())
     ref = w.grad
     assert float((dw.cpu() - ref).abs().max()) <= (1e-4 if prec == "fp32" else 1e-2) * (1 + float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 30, 40, 64, 64), (1, 15, 20, 128, 128), (2, 10, 14, 32, 64),
+                                         (1, 24, 64, 32, 32)])
+def test_conv3x3_wgrad_bn_relu_source(B, H, W, ci, co):
+    """bf16 wgrad whose x operand is relu(bn(y)) applied while the halo is staged (the training path)."""
+    lib = L()
+    torch.manual_seed(3)
+    y = torch.randn(B, ci, H, W).to(torch.bfloat16).float()
+    sc = (torch.rand(ci) + 0.5) * torch.where(torch.rand(ci) < 0.2, -1.0, 1.0)
+    sh = torch.randn(ci) * 0.3
+    x = torch.relu(y * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)).to(torch.bfloat16).float()
+    dy = torch.randn(B, co, H, W).to(torch.bfloat16).float()
+    w = torch.zeros(co, ci, 3, 3, requires_grad=True)
+    F.conv2d(x, w, padding=1).backward(dy)
+    a = lib.make_src(_nhwc(dy, "bf16"), co, H, W, taps=1)
+    b = lib.make_src(_nhwc(y, "bf16"), ci, H, W, taps=9, bn0=(sc.to(DEV), sh.to(DEV)))
+    sp = lib.call("sd_wgrad_splits", lib.SD_BF16, B, H, W, co, 9 * ci)
+    slab = torch.empty(sp * co * 9 * ci, device=DEV)
+    dw = torch.empty(co, ci, 3, 3, device=DEV)
+    lib.call("sd_wgrad_gemm", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, slab.data_ptr(), sp, lib.stream_handle())
+    lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(), lib.stream_handle())
+    ref = w.grad
+    assert float((dw.cpu() - ref).abs().max()) <= 1e-2 * (1 + float(ref.abs().max()))
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])

@@ -95,6 +95,18 @@ def wgrad(B, s, dev):
             L.call("sd_wgrad_reduce", slab.data_ptr(), sp, M, N, L.SD_W_CONV3, ci, dw.data_ptr(), s)
 
         tg, tr = _time(gemm), _time(red)
+        if os.environ.get("SD_WG_DIAG"):  # per-wave cycle counters of a -DWG_EXP=1024 build
+            dbg = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device=dev)
+            L.call("sd_debug_buffer", dbg.data_ptr())
+            gemm()
+            torch.cuda.synchronize()
+            L.call("sd_debug_buffer", None)
+            d = dbg.view(-1, 8, 4).double().cpu()
+            used = d[:, 0, 3] > 0
+            if bool(used.any()):
+                m, ld = d[used, :4].mean((0, 1)), d[used, 4:].mean((0, 1))
+                print(f"  diag cycles/wave: mfma compute {m[0]:.0f} barrier {m[2]:.0f} total {m[3]:.0f} | "
+                      f"loader store {ld[0]:.0f} load {ld[1]:.0f} barrier {ld[2]:.0f} total {ld[3]:.0f}", flush=True)
         flops = 2.0 * P * M * N
         name = L.kernel_name("sd_wgrad_kernel_name", L.SD_BF16, a, b, M, N)
         print(f"wgrad {H}x{W} M={M} ci={ci}: {name} {tg:7.1f} us {flops / tg / 1e6:6.1f} TF | reduce {tr:6.1f} us "
