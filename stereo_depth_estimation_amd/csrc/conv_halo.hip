@@ -840,20 +840,23 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
 // and 9 x-halo fragments (ds_read_b64_tr_b16 pairs) for 36 MFMAs (26 reads per 36 MFMAs; the
 // 2-block kernel reads 22 per 18). The 4 k-steps x 9 taps of a tile run as one straight-line
 // stream of tap-steps with the fragment reads WS_PD tap-steps ahead in a register ring.
-// The halo is laid out with a fixed row pitch of WS_HP pixels (tiles with tw <= 32, th <= 6), so the 9
-// tap offsets of a fragment read are compile-time immediates: no address arithmetic per tap-step (a
-// runtime pitch cost 4 VALU per 4 MFMAs, half the issue slots the 16x16x32 MFMAs leave free).
+// The halo is laid out with a fixed row pitch of HP pixels, so the 9 tap offsets of a fragment read
+// are compile-time immediates: no address arithmetic per tap-step (a runtime pitch cost 4 VALU per 4
+// MFMAs, half the issue slots the 16x16x32 MFMAs leave free). Two layouts, so the staged halo slots
+// (each one is BN+ReLU-transformed by the loaders, whose VALU shares the SIMDs with the MFMA waves and
+// paces the kernel) stay close to the real halo: HP 34 x 6 rows for 4 x 32 tiles (204 slots), HP 22 x 8
+// rows for tiles up to 6 x 20 (176 slots).
 constexpr int WS_TPX = 128;                     // pixels per tile (4 k-steps)
-constexpr int WS_HP = 34, WS_HR = 8;            // halo row pitch (pixels) and rows (th + 2 <= 8, tw + 2 <= 34)
-constexpr int WS_HMAX = 288;                    // halo pixel slots staged (>= WS_HR * WS_HP, 9 pieces per thread)
 constexpr int WS_CI = 64;                       // x channels per block
 constexpr int WS_LD = 64 + 16;                  // 160-B rows (dy and halo): conflict-free transposed reads
 constexpr int WS_PD = 5;                        // tap-steps of fragment read-ahead (4 MFMAs each)
 
+template <int HP, int HR>  // halo row pitch (pixels) and rows: tw + 2 <= HP, th + 2 <= HR
 __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
     constexpr int KS = WS_TPX / 32;
-    constexpr int DY_E = WS_TPX * WS_LD, BUF = DY_E + WS_HMAX * WS_LD;  // elements per LDS buffer
-    constexpr int DYP = WS_TPX * 8 / 256, HXP = WS_HMAX * 8 / 256;     // 16-B pieces per loader thread
+    constexpr int HXP = (HP * HR * 8 + 255) / 256;                      // halo 16-B pieces per loader thread
+    constexpr int DY_E = WS_TPX * WS_LD, BUF = DY_E + HXP * 32 * WS_LD;  // elements per LDS buffer
+    constexpr int DYP = WS_TPX * 8 / 256;                                // dy pieces per loader thread
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -898,7 +901,7 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int px = pix0 + 32 * (i + h);
-                const int hy = px / WS_HP, hx = px - hy * WS_HP;
+                const int hy = px / HP, hx = px - hy * HP;
                 e[h] = (i + h < HXP && hy < p.th + 2 && hx < p.hw) ? (unsigned)(hy << 8 | hx) : 0xffffu;
             }
             hgeo[i / 2] = e[0] | e[1] << 16;
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
         for (int h = 0; h < 2; ++h) {
             const int m = ks * 32 + pc + 8 * h;
             const int hm = m / p.tw;
-            const int px = m < mvalid ? hm * WS_HP + (m - hm * p.tw) : 0;  // dy is 0 past the tile
+            const int px = m < mvalid ? hm * HP + (m - hm * p.tw) : 0;  // dy is 0 past the tile
             xoff[ks][h] = (unsigned)(px * WS_LD + ci0 + 4 * pp) * 2u;
         }
     f32x4 acc[9][4];
@@ -1072,7 +1075,7 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
                     aring[ks & 1][i] = tr_pair(a0, a0 + 8 * WS_LD);
                 }
             }
-            const int toff = ((tap / 3) * WS_HP + tap % 3) * WS_LD;  // compile-time: folds into the ds offset
+            const int toff = ((tap / 3) * HP + tap % 3) * WS_LD;  // compile-time: folds into the ds offset
             bring[j % (WS_PD + 1)] = tr_pair(reinterpret_cast<const __bf16*>(lds + xb[ks][0]) + toff,
                                              reinterpret_cast<const __bf16*>(lds + xb[ks][1]) + toff);
         };
@@ -1339,20 +1342,26 @@ static bool wgrad_ws(int M, int N) {
     return on && M % 64 == 0 && N % 9 == 0 && (N / 9) % WS_CI == 0;
 }
 
-// its tile: th x tw <= 128 pixels, tw <= 32 and th <= 6 (the fixed-pitch halo), minimising the MFMA work
-// (a tile always costs 128 pixels) plus the halo staging over the image
-static HTile wgrad_tile_ws(int H, int W) {
-    HTile best{4, 32, 4};
+// its tile and halo layout: th x tw <= 128 pixels fitting one of the two layouts, minimising the MFMA work
+// (a tile always costs 128 pixels) plus the staged halo slots (each one costs the loaders a transform)
+struct WsTile {
+    int th, tw, hp, hr;
+};
+static WsTile wgrad_tile_ws(int H, int W) {
+    WsTile best{4, 32, 34, 6};
     double best_cost = 1e300;
-    for (int tw = W < 8 ? W : 8; tw <= (W < WS_HP - 2 ? W : WS_HP - 2); ++tw) {
-        if (tw != W && tw != 32 && W % tw) continue;
-        for (int th = 1; th <= H && th * tw <= WS_TPX; ++th) {
-            if (th + 2 > WS_HR) break;
-            const double tiles = (double)cdiv(H, th) * cdiv(W, tw);
-            const double cost = tiles * (WS_TPX + 0.5 * (th + 2) * (tw + 2));
-            if (cost < best_cost) {
-                best_cost = cost;
-                best = {th, tw, 4};
+    const int layouts[2][2] = {{34, 6}, {22, 8}};
+    for (const auto& l : layouts) {
+        const int slots = (l[0] * l[1] * 8 + 255) / 256 * 32;
+        for (int tw = W < 8 ? W : 8; tw <= (W < l[0] - 2 ? W : l[0] - 2); ++tw) {
+            if (tw != W && tw != 32 && W % tw) continue;
+            for (int th = 1; th <= H && th * tw <= WS_TPX && th + 2 <= l[1]; ++th) {
+                const double tiles = (double)cdiv(H, th) * cdiv(W, tw);
+                const double cost = tiles * (WS_TPX + 1.0 * slots);
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best = {th, tw, l[0], l[1]};
+                }
             }
         }
     }
@@ -1361,7 +1370,11 @@ static HTile wgrad_tile_ws(int H, int W) {
 
 int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
     const bool ws = wgrad_ws(M, N);
-    const HTile t = ws ? wgrad_tile_ws(H, W) : wgrad_tile(H, W);
+    HTile t = wgrad_tile(H, W);
+    if (ws) {
+        const WsTile w = wgrad_tile_ws(H, W);
+        t = {w.th, w.tw, 4, 32};
+    }
     const int nblk = ws ? (N / 9 / WS_CI) * (M / 64) : cdiv(N / 9, CK) * (M == 32 ? 1 : M / 64);
     const int nt = cdiv(W, t.tw) * cdiv(H, t.th) * batch;
     static const int blocks = [] {  // SD_WG_BLOCKS: total split-K blocks (A/B runs)
@@ -1374,14 +1387,17 @@ int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
     return splits < 1 ? 1 : splits;
 }
 
-const char* sd_halo_wgrad_name(int M, int N, int c0) {
-    return M == 32 ? "k_halo_wgrad<32>" : wgrad_ws(M, N) && c0 % WS_CI == 0 ? "k_halo_wgrad_ws" : "k_halo_wgrad<64>";
+const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W) {
+    if (M == 32) return "k_halo_wgrad<32>";
+    if (!(wgrad_ws(M, N) && c0 % WS_CI == 0)) return "k_halo_wgrad<64>";
+    return wgrad_tile_ws(H, W).hp == 34 ? "k_halo_wgrad_ws<34, 6>" : "k_halo_wgrad_ws<22, 8>";
 }
 
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
                   hipStream_t st) {
     const bool ws = wgrad_ws(M, N) && b.chans[0] % WS_CI == 0;  // one source per 64-channel block
-    const HTile t = ws ? wgrad_tile_ws(H, W) : wgrad_tile(H, W);
+    const WsTile wt = wgrad_tile_ws(H, W);
+    const HTile t = ws ? HTile{wt.th, wt.tw, 4, 32} : wgrad_tile(H, W);
     HWgArgs p;
     p.dy = (const __bf16*)a.ptr[0];
     p.x = make_halo_src(b);
@@ -1402,9 +1418,12 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
     if (ws) {
         const int ncc = p.x.ctot / WS_CI;
         p.xcd = halo_xcd_enabled() && (ncc * splits * (M / 64)) % 8 == 0;
-        SD_REQUIRE(t.th + 2 <= WS_HR && t.tw + 2 <= WS_HP && t.th * t.tw <= WS_TPX, "sd_wgrad_gemm(halo ws): tile %dx%d",
+        SD_REQUIRE(t.th + 2 <= wt.hr && t.tw + 2 <= wt.hp && t.th * t.tw <= WS_TPX, "sd_wgrad_gemm(halo ws): tile %dx%d",
                    t.th, t.tw);
-        hipLaunchKernelGGL(k_halo_wgrad_ws, dim3(ncc, splits, M / 64), dim3(512), 0, st, p);
+        if (wt.hp == 34)
+            hipLaunchKernelGGL((k_halo_wgrad_ws<34, 6>), dim3(ncc, splits, M / 64), dim3(512), 0, st, p);
+        else
+            hipLaunchKernelGGL((k_halo_wgrad_ws<22, 8>), dim3(ncc, splits, M / 64), dim3(512), 0, st, p);
         return sd_check_launch("sd_wgrad_gemm(halo ws)");
     }
     p.xcd = halo_xcd_enabled() && (cdiv(p.x.ctot, CK) * splits * (M == 32 ? 1 : M / 64)) % 8 == 0;

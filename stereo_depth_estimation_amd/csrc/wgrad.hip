@@ -259,13 +259,13 @@ int sd_fast_wgrad_gemm(const sd_src& a, const sd_src& b, int batch, int H, int W
 bool sd_halo_wgrad_ok(const sd_src& a, const sd_src& b, int M);
 bool sd_halo_wgrad_shape(int M, int N);
 int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N);
-const char* sd_halo_wgrad_name(int M, int N, int c0);
+const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W);
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
                   hipStream_t st);
 
 extern "C" const char* sd_wgrad_kernel_name(int dtype, const sd_src* a, const sd_src* b, int M, int N) {
     static thread_local char buf[96];
-    if (dtype == SD_BF16 && a && b && sd_halo_wgrad_ok(*a, *b, M)) return sd_halo_wgrad_name(M, N, b->chans[0]);
+    if (dtype == SD_BF16 && a && b && sd_halo_wgrad_ok(*a, *b, M)) return sd_halo_wgrad_name(M, N, b->chans[0], a->H, a->W);
     if (dtype == SD_BF16 && a && b && !a->pool && !b->pool) return sd_fast_wgrad_name(M, N);
     const WCfg c = pick_wcfg(M, N);
     snprintf(buf, sizeof(buf), "k_wgemm<%s, %d, %d, 2, 2>", dtype == SD_BF16 ? "__bf16" : "float", c.bm, c.bn);

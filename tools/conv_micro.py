@@ -104,9 +104,13 @@ def wgrad(B, s, dev):
             d = dbg.view(-1, 8, 4).double().cpu()
             used = d[:, 0, 3] > 0
             if bool(used.any()):
+                raw = dbg.view(-1, 8, 4).cpu()
+                vm = (raw[used, 4:, 1] >> 32).double().mean()
+                d[:, 4:, 1] = (raw[:, 4:, 1] & 0xFFFFFFFF).double()
                 m, ld = d[used, :4].mean((0, 1)), d[used, 4:].mean((0, 1))
                 print(f"  diag cycles/wave: mfma compute {m[0]:.0f} barrier {m[2]:.0f} total {m[3]:.0f} | "
-                      f"loader store {ld[0]:.0f} load {ld[1]:.0f} barrier {ld[2]:.0f} total {ld[3]:.0f}", flush=True)
+                      f"loader store {ld[0]:.0f} (of it vmcnt wait {vm:.0f}) load {ld[1]:.0f} barrier {ld[2]:.0f} "
+                      f"total {ld[3]:.0f}", flush=True)
         flops = 2.0 * P * M * N
         name = L.kernel_name("sd_wgrad_kernel_name", L.SD_BF16, a, b, M, N)
         print(f"wgrad {H}x{W} M={M} ci={ci}: {name} {tg:7.1f} us {flops / tg / 1e6:6.1f} TF | reduce {tr:6.1f} us "
