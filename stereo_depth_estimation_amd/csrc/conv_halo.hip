@@ -345,7 +345,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             for (int i = 0; i < HP; ++i) {  // every piece lands inside the halo region
                 const int item = ltid + i * 256;
                 *reinterpret_cast<uint4*>(hx + ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8) =
-                    halo_finish(set_of(S).hc, (set_of(S).m >> i) & 1u, set_of(S).hr[i]);
+                    halo_finish_pk(set_of(S).hc, (set_of(S).m >> i) & 1u, set_of(S).hr[i]);
             }
             if (!wconst) {
                 store_w(buf);
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
         for (int i = 0; i < HP_PER_THREAD; ++i) {  // every piece lands inside the HMAX-pixel region
             const int item = tid + i * 256;
             *reinterpret_cast<uint4*>(hxs + wg_pixel(item) * XW_LD + wg_piece(item) * 8) =
-                halo_finish(hc, (xmask[S] >> i) & 1u, xr[S][i]);
+                halo_finish_pk(hc, (xmask[S] >> i) & 1u, xr[S][i]);
         }
     };
     constexpr std::integral_constant<int, 0> S0{};
