@@ -824,19 +824,18 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
 
 
 // =====================================================================================
-// wgrad, warp-specialised: M % 64 == 0 and x channels % 64 == 0 (every M % 64 layer but enc2.0)
+// wgrad, warp-specialised: M = 32 or M % 64 == 0, x channels % 32 == 0 (every 3x3 wgrad but enc1.0)
 // =====================================================================================
-// One 512-thread block per CU. A block owns 64 dy channels (rows of dW) x 64 x channels x 9 taps
+// One 512-thread block per CU. A block owns COUT dy channels (rows of dW) x CIB x channels x 9 taps
 // and a range of 128-pixel tiles (split-K). Waves 4-7 stage tile t+1 (the dy rows, and the x halo
 // through BN+ReLU) into one LDS buffer while waves 0-3 run tile t's MFMAs from the other, one
 // barrier per tile: the one-role-per-wave layout of k_halo_conv. (k_halo_wgrad interleaves both
 // roles in every wave at 2 blocks per CU; timing runs with either role removed measured its MFMA
 // phase alone at 74 us of 136 us for 120x160x64x64: the staging was not hidden.)
-// MFMA wave w owns all 64 dy channels (4 16-row tiles) x the 16 x channels 16w..16w+15 x 9 taps:
-// 36 accumulators of v_mfma_f32_16x16x32_bf16 (144 registers). Per 32-pixel k-step it reads 4 dy
-// and 9 x-halo fragments (ds_read_b64_tr_b16 pairs) for 36 MFMAs (26 reads per 36 MFMAs; the
-// 2-block kernel reads 22 per 18). The 4 k-steps x 9 taps of a tile run as one straight-line
-// stream of tap-steps with the fragment reads WS_PD tap-steps ahead in a register ring.
+// MFMA waves: CIB/16 x-channel groups of 16 x 4/(CIB/16) dy-channel groups; a wave owns RM 16-row
+// dy tiles x 16 x channels x 9 taps of v_mfma_f32_16x16x32_bf16 accumulators (RM = 4 at 64 x 64:
+// 144 registers, 26 fragment reads per 36 MFMAs per k-step). The 4 k-steps x 9 taps of a tile run as
+// one straight-line stream of tap-steps with the fragment reads WS_PD tap-steps ahead in a register ring.
 // The halo is laid out with a fixed row pitch of HP pixels, so the 9 tap offsets of a fragment read
 // are compile-time immediates: no address arithmetic per tap-step (a runtime pitch cost 4 VALU per 4
 // MFMAs, half the issue slots the 16x16x32 MFMAs leave free). Two layouts, so the staged halo slots
@@ -844,16 +843,25 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
 // paces the kernel) stay close to the real halo: HP 34 x 6 rows for 4 x 32 tiles (204 slots), HP 22 x 8
 // rows for tiles up to 6 x 20 (176 slots).
 constexpr int WS_TPX = 128;                     // pixels per tile (4 k-steps)
-constexpr int WS_CI = 64;                       // x channels per block
-constexpr int WS_LD = 64 + 16;                  // 160-B rows (dy and halo): conflict-free transposed reads
-constexpr int WS_PD = 5;                        // tap-steps of fragment read-ahead (4 MFMAs each)
+constexpr int WS_PD = 5;                        // tap-steps of fragment read-ahead
+#ifndef WS_PRIO
+#define WS_PRIO 0
+#endif
 
-template <int HP, int HR>  // halo row pitch (pixels) and rows: tw + 2 <= HP, th + 2 <= HR
-__global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
+// blocks per CU: two for the 32 x 32-channel configuration (72 KB of LDS, <= 128 registers), whose
+// tiles carry little MFMA work and need more loads in flight; one otherwise
+__host__ __device__ constexpr int ws_blocks_per_cu(int cout, int cib) { return cout == 32 && cib == 32 ? 2 : 1; }
+
+template <int COUT, int CIB, int HP, int HR>  // dy / x channels per block; halo pitch and rows (tw+2 <= HP, th+2 <= HR)
+__global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_wgrad_ws(const HWgArgs p) {
     constexpr int KS = WS_TPX / 32;
-    constexpr int HXP = (HP * HR * 8 + 255) / 256;                      // halo 16-B pieces per loader thread
-    constexpr int DY_E = WS_TPX * WS_LD, BUF = DY_E + HXP * 32 * WS_LD;  // elements per LDS buffer
-    constexpr int DYP = WS_TPX * 8 / 256;                                // dy pieces per loader thread
+    constexpr int NCI = CIB / 16, NCO = 4 / NCI, RM = COUT / 16 / NCO;  // wave grid and 16-row tiles per wave
+    constexpr int DPP = COUT / 8, XPP = CIB / 8;                       // 16-B pieces per pixel (dy, x)
+    constexpr int DLD = COUT + 16, XLD = CIB + 16;                     // 96 / 160-B rows: conflict-free tr reads
+    constexpr int DYP = WS_TPX * DPP / 256;                            // dy pieces per loader thread
+    constexpr int HXP = (HP * HR * XPP + 255) / 256;                   // halo pieces per loader thread
+    constexpr int DY_E = WS_TPX * DLD, BUF = DY_E + HXP * (256 / XPP) * XLD;  // elements per LDS buffer
+    static_assert(RM >= 1 && NCI * NCO == 4, "wave grid");
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -869,24 +877,26 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
         zb = r % gridDim.z;
         split = r / gridDim.z;
     }
-    const int mb = zb * 64;
+    const int mb = zb * COUT;
     const int t_begin = split * p.tiles_per_split;
     const int ntile = max(0, min(p.ntiles, t_begin + p.tiles_per_split) - t_begin);
     const int mvalid = p.th * p.tw;
 
     if (is_loader) {
         // =========================================================== loader waves
-        // item = ltid + 256 i -> (pixel item >> 3, 16-B piece ltid & 7): the piece (8 channels) is fixed per
-        // thread, and an 8-lane ds_write_b128 group covers one pixel's 8 pieces at the 10-slot row
-        // stride: conflict-free
-        const int ltid = tid - 256, piece = ltid & 7, pix0 = ltid >> 3;
+        if (WS_PRIO) __builtin_amdgcn_s_setprio(WS_PRIO);
+        // item = ltid + 256 i -> (pixel item / P, 16-B piece ltid % P) for P pieces per pixel: the piece is
+        // fixed per thread; an 8-lane ds_write_b128 group covers one pixel's 8 pieces at the 10-slot row
+        // stride (64 channels: conflict-free) or two pixels' 4 at the 6-slot stride
+        const int ltid = tid - 256;
+        const int dpiece = ltid % DPP, dpix0 = ltid / DPP, xpiece = ltid % XPP, xpix0 = ltid / XPP;
         unsigned dyrc[(DYP + 1) / 2], hgeo[(HXP + 1) / 2];  // (row << 8 | col), 0xffff past the tile / halo
 #pragma unroll
         for (int i = 0; i < DYP; i += 2) {
             unsigned e[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int m = pix0 + 32 * (i + h);
+                const int m = dpix0 + (256 / DPP) * (i + h);
                 const int hm = m / p.tw;
                 e[h] = (i + h < DYP && m < mvalid) ? (unsigned)(hm << 8 | (m - hm * p.tw)) : 0xffffu;
             }
@@ -897,17 +907,17 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
             unsigned e[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int px = pix0 + 32 * (i + h);
+                const int px = xpix0 + (256 / XPP) * (i + h);
                 const int hy = px / HP, hx = px - hy * HP;
                 e[h] = (i + h < HXP && hy < p.th + 2 && hx < p.hw) ? (unsigned)(hy << 8 | hx) : 0xffffu;
             }
             hgeo[i / 2] = e[0] | e[1] << 16;
         }
-        // the block's 64 x channels come from one source (the dispatcher requires chans[0] % 64 == 0)
-        const bool src1 = cc * WS_CI >= p.x.c0;
+        // the block's CIB x channels come from one source (the dispatcher requires chans[0] % CIB == 0)
+        const bool src1 = cc * CIB >= p.x.c0;
         const __bf16* xsrc = src1 ? p.x.p1 : p.x.p0;
         const int xC = src1 ? p.x.c1 : p.x.c0;
-        const HaloCol hc = halo_col(p.x, cc * WS_CI + piece * 8, p.dy);  // this thread's 8 channels (BN affine)
+        const HaloCol hc = halo_col(p.x, cc * CIB + xpiece * 8, p.dy);  // this thread's 8 channels (BN affine)
         // Per-piece element offsets from the tile origin (h0, w0), fixed for the launch: a piece's buffer
         // offset is then one add, its bounds test four compares against per-tile scalars, and a piece
         // outside the image / tile gets an offset past the buffer's range, which the buffer load returns
@@ -916,7 +926,7 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
 #pragma unroll
         for (int i = 0; i < DYP; ++i) {
             const unsigned rc = (dyrc[i / 2] >> (16 * (i & 1))) & 0xffffu;
-            dpo[i] = ((int)(rc >> 8) * p.W + (int)(rc & 0xff)) * p.M + mb + piece * 8;
+            dpo[i] = ((int)(rc >> 8) * p.W + (int)(rc & 0xff)) * p.M + mb + dpiece * 8;
         }
 #pragma unroll
         for (int i = 0; i < HXP; ++i) {
@@ -972,11 +982,11 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
             __bf16* hxs = dys + DY_E;
 #pragma unroll
             for (int i = 0; i < DYP; ++i)  // out-of-range pieces were loaded as zeros
-                *reinterpret_cast<uint4*>(dys + (pix0 + 32 * i) * WS_LD + piece * 8) = q.d[i];
+                *reinterpret_cast<uint4*>(dys + (dpix0 + (256 / DPP) * i) * DLD + dpiece * 8) = q.d[i];
 #pragma unroll
             for (int i = 0; i < HXP; ++i)
-                *reinterpret_cast<uint4*>(hxs + (pix0 + 32 * i) * WS_LD + piece * 8) =
-                    halo_finish_pk(hc, (q.xm >> i) & 1u, q.x[i]);
+                *reinterpret_cast<uint4*>(hxs + (xpix0 + (256 / XPP) * i) * XLD + xpiece * 8) =
+                    (WG_EXP & 2048) ? q.x[i] : halo_finish_pk(hc, (q.xm >> i) & 1u, q.x[i]);
         };
         // tile i is in set i & 1 from its load until its store, which happens one tile ahead of the MFMA
         // waves; each set is refilled right after its store, so two tiles' loads are in flight. Loads are
@@ -984,8 +994,6 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
         // cannot count vmcnt and drains every load before each store
         constexpr bool DG = (WG_EXP & 1024) != 0;
         unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t1 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
-#define WS_T0() if (DG) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); t0 = __builtin_amdgcn_s_memtime(); }
-#define WS_T1(acc_) if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); acc_ += t1 - t0; }
         load(sa, t_begin);
         load(sb, t_begin + 1);
         if (ntile > 0) store(sa, 0);
@@ -994,19 +1002,17 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
         for (int i = 0; i < ntile; i += 2) {
             if (DG) t0 = __builtin_amdgcn_s_memtime();
             if (i + 1 < ntile) store(sb, 1);
-            WS_T1(t_st)
+            if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); t_st += t1 - t0; }
             load(sb, t_begin + i + 3);
-            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; }
-            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; t0 = t1; }
             __syncthreads();
             if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
             if (i + 1 >= ntile) break;
             if (DG) t0 = __builtin_amdgcn_s_memtime();
             if (i + 2 < ntile) store(sa, 0);
-            WS_T1(t_st)
+            if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); t_st += t1 - t0; }
             load(sa, t_begin + i + 4);
-            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; }
-            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; t0 = t1; }
             __syncthreads();
             if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
         }
@@ -1017,15 +1023,13 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
             d[2] = t_br;
             d[3] = __builtin_amdgcn_s_memtime() - t_all;
         }
-#undef WS_T0
-#undef WS_T1
         return;
     }
 
     // =============================================================== MFMA waves
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
     const int pc = 16 * (g >> 1) + 4 * (g & 1) + q;  // pixel within the k-step (0..23), +8 for the 2nd read
-    const int ci0 = 16 * wid;
+    const int ci0 = 16 * (wid % NCI), co0 = (wid / NCI) * (COUT / NCO);
     // byte offsets (within the halo region) of this lane's two halo rows of each k-step at tap (0,0)
     unsigned xoff[KS][2];
 #pragma unroll
@@ -1035,25 +1039,25 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
             const int m = ks * 32 + pc + 8 * h;
             const int hm = m / p.tw;
             const int px = m < mvalid ? hm * HP + (m - hm * p.tw) : 0;  // dy is 0 past the tile
-            xoff[ks][h] = (unsigned)(px * WS_LD + ci0 + 4 * pp) * 2u;
+            xoff[ks][h] = (unsigned)(px * XLD + ci0 + 4 * pp) * 2u;
         }
-    f32x4 acc[9][4];
+    f32x4 acc[9][RM];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < RM; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     constexpr int NSTEP = KS * 9;
     bf16x8 bring[WS_PD + 1];
-    bf16x8 aring[2][4];
+    bf16x8 aring[2][RM];
     const char* lds = reinterpret_cast<const char*>(smem);
     constexpr bool DG = (WG_EXP & 1024) != 0;
     unsigned long long t_cp = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     for (int it = 0; it < ntile; ++it) {
         if (DG) t0 = __builtin_amdgcn_s_memtime();
-        const unsigned bufb = (unsigned)((it & 1) * BUF * 2);                           // byte offset of this buffer
-        unsigned abase = bufb + (unsigned)(pc * WS_LD + 4 * pp) * 2u;
+        const unsigned bufb = (unsigned)((it & 1) * BUF * 2);  // byte offset of this buffer
+        unsigned abase = bufb + (unsigned)(pc * DLD + co0 + 4 * pp) * 2u;
         asm volatile("" : "+v"(abase));
         unsigned xb[KS][2];  // this tile's read addresses; opaque so the compiler keeps them per tile
 #pragma unroll
@@ -1067,29 +1071,29 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
             const int ks = j / 9, tap = j - ks * 9;
             if (tap == 0) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const __bf16* a0 = reinterpret_cast<const __bf16*>(lds + abase) + ks * 32 * WS_LD + i * 16;
-                    aring[ks & 1][i] = tr_pair(a0, a0 + 8 * WS_LD);
+                for (int i = 0; i < RM; ++i) {
+                    const __bf16* a0 = reinterpret_cast<const __bf16*>(lds + abase) + ks * 32 * DLD + i * 16;
+                    aring[ks & 1][i] = tr_pair(a0, a0 + 8 * DLD);
                 }
             }
-            const int toff = ((tap / 3) * HP + tap % 3) * WS_LD;  // compile-time: folds into the ds offset
+            const int toff = ((tap / 3) * HP + tap % 3) * XLD;  // compile-time: folds into the ds offset
             bring[j % (WS_PD + 1)] = tr_pair(reinterpret_cast<const __bf16*>(lds + xb[ks][0]) + toff,
                                              reinterpret_cast<const __bf16*>(lds + xb[ks][1]) + toff);
         };
         if (!(WG_EXP & 64)) {
 #pragma unroll
-        for (int j = 0; j < WS_PD; ++j) issue(j);
+            for (int j = 0; j < WS_PD; ++j) issue(j);
 #pragma unroll
-        for (int j = 0; j < NSTEP; ++j) {
-            if (j + WS_PD < NSTEP) issue(j + WS_PD);
-            __builtin_amdgcn_sched_barrier(0);
-            const int ks = j / 9, tap = j - ks * 9;
+            for (int j = 0; j < NSTEP; ++j) {
+                if (j + WS_PD < NSTEP) issue(j + WS_PD);
+                __builtin_amdgcn_sched_barrier(0);
+                const int ks = j / 9, tap = j - ks * 9;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aring[ks & 1][i], bring[j % (WS_PD + 1)], acc[tap][i],
-                                                                     0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+                for (int i = 0; i < RM; ++i)
+                    acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aring[ks & 1][i], bring[j % (WS_PD + 1)],
+                                                                         acc[tap][i], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         if (DG) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -1106,16 +1110,16 @@ __global__ __launch_bounds__(512) void k_halo_wgrad_ws(const HWgArgs p) {
         d[2] = t_br;
         d[3] = __builtin_amdgcn_s_memtime() - t_all;
     }
-    // slab[split][co][tap*ctot + cc*64 + ci]   (C layout 16x16: row = 4*(lane>>4) + r, col = lane&15)
+    // slab[split][co][tap*ctot + cc*CIB + ci]   (C layout 16x16: row = 4*(lane>>4) + r, col = lane&15)
     float* slab = p.slab + (size_t)split * p.M * p.N;
-    const int ci = cc * WS_CI + ci0 + (lane & 15);
+    const int ci = cc * CIB + ci0 + (lane & 15);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int co = mb + i * 16 + 4 * (lane >> 4) + r;
+                const int co = mb + co0 + i * 16 + 4 * (lane >> 4) + r;
                 slab[(size_t)co * p.N + tap * p.x.ctot + ci] = acc[tap][i][r];
             }
 }
@@ -1329,14 +1333,24 @@ extern "C" int sd_debug_buffer(void* p) {
     return 0;
 }
 
-// warp-specialised wgrad (k_halo_wgrad_ws) for M % 64 == 0 with x channels % 64 == 0; SD_WG_WS=0 keeps
-// k_halo_wgrad (A/B runs)
-static bool wgrad_ws(int M, int N) {
+// warp-specialised wgrad (k_halo_wgrad_ws): dy channels per block COUT = 64 (M % 64 == 0) or 32 (M == 32),
+// x channels per block CIB = 64 or 32 (the channel count and the first source's width divisible by it;
+// c0 < 0: unknown, sizing only). 0: not applicable (enc1.0's 8-channel input), k_halo_wgrad runs.
+// SD_WG_WS=0 keeps k_halo_wgrad everywhere (A/B runs).
+struct WsCfg {
+    int cout, cib;
+};
+static WsCfg wgrad_ws(int M, int N, int c0 = -1) {
     static const bool on = [] {
         const char* e = getenv("SD_WG_WS");
         return !(e && atoi(e) == 0);
     }();
-    return on && M % 64 == 0 && N % 9 == 0 && (N / 9) % WS_CI == 0;
+    const int ctot = N / 9;
+    WsCfg c{M % 64 == 0 ? 64 : (M == 32 ? 32 : 0), 0};
+    if (!on || c.cout == 0 || N % 9) return {0, 0};
+    if (ctot % 64 == 0 && (c0 < 0 || c0 % 64 == 0)) c.cib = 64;
+    else if (ctot % 32 == 0 && (c0 < 0 || c0 % 32 == 0)) c.cib = 32;
+    return c.cib ? c : WsCfg{0, 0};
 }
 
 // its tile and halo layout: th x tw <= 128 pixels fitting one of the two layouts, minimising the MFMA work
@@ -1366,35 +1380,46 @@ static WsTile wgrad_tile_ws(int H, int W) {
 }
 
 int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
-    const bool ws = wgrad_ws(M, N);
+    const WsCfg ws = wgrad_ws(M, N);
     HTile t = wgrad_tile(H, W);
-    if (ws) {
+    if (ws.cib) {
         const WsTile w = wgrad_tile_ws(H, W);
         t = {w.th, w.tw, 4, 32};
     }
-    const int nblk = ws ? (N / 9 / WS_CI) * (M / 64) : cdiv(N / 9, CK) * (M == 32 ? 1 : M / 64);
+    const int nblk = ws.cib ? (N / 9 / ws.cib) * (M / ws.cout) : cdiv(N / 9, CK) * (M == 32 ? 1 : M / 64);
     const int nt = cdiv(W, t.tw) * cdiv(H, t.th) * batch;
     static const int blocks = [] {  // SD_WG_BLOCKS: total split-K blocks (A/B runs)
         const char* e = getenv("SD_WG_BLOCKS");
         return e && atoi(e) > 0 ? atoi(e) : 512;
     }();
     // one round of blocks: 2 per CU for k_halo_wgrad (LDS, registers), 1 per CU for the warp-specialised one
-    int splits = cdiv(ws ? PERSIST_BLOCKS : blocks, nblk);
+    int splits = cdiv(ws.cib ? PERSIST_BLOCKS * ws_blocks_per_cu(ws.cout, ws.cib) : blocks, nblk);
     if (splits > nt) splits = nt;
     return splits < 1 ? 1 : splits;
 }
 
 const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W) {
-    if (M == 32) return "k_halo_wgrad<32>";
-    if (!(wgrad_ws(M, N) && c0 % WS_CI == 0)) return "k_halo_wgrad<64>";
-    return wgrad_tile_ws(H, W).hp == 34 ? "k_halo_wgrad_ws<34, 6>" : "k_halo_wgrad_ws<22, 8>";
+    static thread_local char buf[64];
+    const WsCfg ws = wgrad_ws(M, N, c0);
+    if (!ws.cib) return M == 32 ? "k_halo_wgrad<32>" : "k_halo_wgrad<64>";
+    const WsTile t = wgrad_tile_ws(H, W);
+    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d>", ws.cout, ws.cib, t.hp, t.hr);
+    return buf;
+}
+
+template <int COUT, int CIB>
+static void launch_wgrad_ws(int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
+    if (hp == 34)
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6>), grid, dim3(512), 0, st, p);
+    else
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8>), grid, dim3(512), 0, st, p);
 }
 
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
                   hipStream_t st) {
-    const bool ws = wgrad_ws(M, N) && b.chans[0] % WS_CI == 0;  // one source per 64-channel block
+    const WsCfg ws = wgrad_ws(M, N, b.chans[0]);  // one source per block of x channels
     const WsTile wt = wgrad_tile_ws(H, W);
-    const HTile t = ws ? HTile{wt.th, wt.tw, 4, 32} : wgrad_tile(H, W);
+    const HTile t = ws.cib ? HTile{wt.th, wt.tw, 4, 32} : wgrad_tile(H, W);
     HWgArgs p;
     p.dy = (const __bf16*)a.ptr[0];
     p.x = make_halo_src(b);
@@ -1412,15 +1437,16 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
     p.N = N;
     p.slab = slab;
     p.dbg = g_wg_dbg;
-    if (ws) {
-        const int ncc = p.x.ctot / WS_CI;
-        p.xcd = halo_xcd_enabled() && (ncc * splits * (M / 64)) % 8 == 0;
+    if (ws.cib) {
+        const int ncc = p.x.ctot / ws.cib;
+        p.xcd = halo_xcd_enabled() && (ncc * splits * (M / ws.cout)) % 8 == 0;
         SD_REQUIRE(t.th + 2 <= wt.hr && t.tw + 2 <= wt.hp && t.th * t.tw <= WS_TPX, "sd_wgrad_gemm(halo ws): tile %dx%d",
                    t.th, t.tw);
-        if (wt.hp == 34)
-            hipLaunchKernelGGL((k_halo_wgrad_ws<34, 6>), dim3(ncc, splits, M / 64), dim3(512), 0, st, p);
-        else
-            hipLaunchKernelGGL((k_halo_wgrad_ws<22, 8>), dim3(ncc, splits, M / 64), dim3(512), 0, st, p);
+        const dim3 grid(ncc, splits, M / ws.cout);
+        if (ws.cout == 64 && ws.cib == 64) launch_wgrad_ws<64, 64>(wt.hp, grid, st, p);
+        else if (ws.cout == 64) launch_wgrad_ws<64, 32>(wt.hp, grid, st, p);
+        else if (ws.cib == 64) launch_wgrad_ws<32, 64>(wt.hp, grid, st, p);
+        else launch_wgrad_ws<32, 32>(wt.hp, grid, st, p);
         return sd_check_launch("sd_wgrad_gemm(halo ws)");
     }
     p.xcd = halo_xcd_enabled() && (cdiv(p.x.ctot, CK) * splits * (M == 32 ? 1 : M / 64)) % 8 == 0;

@@ -160,7 +160,10 @@ def test_conv3x3_dual_source_and_dgrad_split(prec, B, H, W, c0, c1, co):
                                          # warp-specialised wgrad (M % 64, x channels % 64): 2 x-channel blocks,
                                          # 2 dy blocks, ragged tiles, many tiles per split
                                          (2, 30, 40, 128, 64), (1, 13, 50, 64, 128), (3, 17, 33, 64, 64),
-                                         (1, 120, 160, 64, 64)])
+                                         (1, 120, 160, 64, 64),
+                                         # M = 32 / 32-channel x blocks (the full-resolution layers)
+                                         (2, 12, 40, 32, 32), (1, 24, 64, 64, 32), (2, 15, 20, 32, 64),
+                                         (1, 48, 64, 32, 32)])
 def test_conv3x3_wgrad(prec, B, H, W, ci, co):
     lib = L()
     torch.manual_seed(2)
@@ -181,7 +184,7 @@ def test_conv3x3_wgrad(prec, B, H, W, ci, co):
 
 
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 30, 40, 64, 64), (1, 15, 20, 128, 128), (2, 10, 14, 32, 64),
-                                         (1, 24, 64, 32, 32)])
+                                         (1, 24, 64, 32, 32), (1, 16, 64, 64, 32)])
 def test_conv3x3_wgrad_bn_relu_source(B, H, W, ci, co):
     """bf16 wgrad whose x operand is relu(bn(y)) applied while the halo is staged (the training path)."""
     lib = L()

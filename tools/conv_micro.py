@@ -71,7 +71,8 @@ def run(B, H, W, ci, co, stats, s, dev, n=20):
 
 
 WGRAD_LAYERS = [  # (H, W, dy channels M, x channels ci)
-    (240, 320, 32, 32), (240, 320, 32, 64), (120, 160, 64, 64), (60, 80, 128, 128), (30, 40, 256, 256)]
+    (240, 320, 32, 32), (240, 320, 32, 64), (120, 160, 64, 32), (120, 160, 64, 64), (60, 80, 128, 128),
+    (30, 40, 256, 256)]
 
 
 def wgrad(B, s, dev):
