@@ -270,12 +270,15 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         // Loads are unconditional (chunks past the end re-read valid addresses and are never
         // stored), which keeps the in-order vmcnt bookkeeping static: each store waits only for
         // its own set.
-        // LS register sets: chunk j lives in set j % LS between its load and its store, so LS chunks'
-        // halo loads are in flight while the MFMA waves compute another. N = 32 layers on 8x32 tiles
-        // (full resolution, HBM-bound, one or two short chunks per item) keep 3 in flight, 4 for the
-        // 5-k-step CK = 8 chunks of the network input; elsewhere the 2 sets cover an HBM round trip
-        // with longer items, and the registers are spoken for.
-        constexpr int LS = NT == 1 && CK == 8 ? 4 : (NT == 1 && RT == 2 ? 3 : 2);
+        // LS register sets: chunk j lives in set j % LS between its load and its store, so up to LS chunks'
+        // halo loads are in flight while the MFMA waves compute another.
+        // UNCOND: the N = 32 instances (full resolution, HBM-bound) keep their loads unconditional so vmcnt stays
+        // countable and every set's loads stay in flight until its store; that gives the 8-channel input 3
+        // sets' cover at LS = 4 and made LS = 3 spill, so LS = 2 there. The N % 64 instances measured 2-5 %
+        // slower with unconditional loads (more requests in flight beside the MFMA-bound body) and keep the
+        // guarded form.
+        constexpr bool UNCOND = NT == 1;
+        constexpr int LS = NT == 1 && CK == 8 ? 4 : 2;
         constexpr int UF = LS == 3 ? 6 : LS;  // unroll: both the set (j % LS) and the buffer (j & 1) static
         // one object per set (an array of sets past ~256 B stays in scratch instead of registers)
         struct HSet {
@@ -350,7 +353,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             if (!wconst) {
                 store_w(buf);
                 if (++w_cc == nchunks) w_cc = 0;
-                load_w(w_cc);
             }
         };
         constexpr std::integral_constant<int, 0> S0{};
@@ -371,16 +373,25 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             if constexpr (LS >= 3) load(S2);
             if constexpr (LS >= 4) load(S3);
             store(S0, 0);
+            if (!wconst) load_w(w_cc);  // chunk 1's weights
             load(S0);  // chunk LS
         }
         __syncthreads();
         // iteration g: the MFMA waves read buffer g&1; store chunk g+1 (set (g+1) % LS) into the other
         // buffer and refill that set with chunk g+1+LS. Unrolled by LS so set and buffer indices are
         // static; returns false after the last iteration's barrier.
+        // The loads are unconditional (past the last chunk they re-read valid addresses and are never stored):
+        // a load issued on only some paths makes the compiler's vmcnt bookkeeping drain every outstanding load
+        // before each store, which left one chunk of latency cover instead of LS
         auto iter = [&](auto U, int g) __attribute__((always_inline)) {
             constexpr int s_ = (decltype(U)::value + 1) % LS;
-            if (g + 1 < total) {
+            if constexpr (UNCOND) {
+                if (g + 1 < total) store(std::integral_constant<int, s_>{}, (decltype(U)::value + 1) & 1);
+                if (!wconst) load_w(w_cc);
+                load(std::integral_constant<int, s_>{});
+            } else if (g + 1 < total) {
                 store(std::integral_constant<int, s_>{}, (decltype(U)::value + 1) & 1);
+                if (!wconst) load_w(w_cc);
                 load(std::integral_constant<int, s_>{});
             }
             __syncthreads();
