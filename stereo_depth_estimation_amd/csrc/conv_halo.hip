@@ -192,6 +192,7 @@ struct HFwdArgs {
     int n_split;
     float* stats;         // [gper][N] float2 (sum, sumsq of the stored bf16 values)
     int xcd;              // 1: XCD-contiguous block numbering (grid % 8 == 0)
+    unsigned long long* dbg;  // timing-diagnostic builds only (WG_EXP & 1024): per-wave cycle counters
 };
 
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
@@ -383,18 +384,34 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         // The loads are unconditional (past the last chunk they re-read valid addresses and are never stored):
         // a load issued on only some paths makes the compiler's vmcnt bookkeeping drain every outstanding load
         // before each store, which left one chunk of latency cover instead of LS
+        constexpr bool DG = (WG_EXP & 1024) != 0;
+        unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
+        auto stamp = [&](unsigned long long& acc_) __attribute__((always_inline)) {
+            if (DG) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+                acc_ += t1 - t0;
+                t0 = t1;
+            }
+        };
         auto iter = [&](auto U, int g) __attribute__((always_inline)) {
             constexpr int s_ = (decltype(U)::value + 1) % LS;
+            if (DG) t0 = __builtin_amdgcn_s_memtime();
             if constexpr (UNCOND) {
                 if (g + 1 < total) store(std::integral_constant<int, s_>{}, (decltype(U)::value + 1) & 1);
+                stamp(t_st);
                 if (!wconst) load_w(w_cc);
                 load(std::integral_constant<int, s_>{});
+                stamp(t_ld);
             } else if (g + 1 < total) {
                 store(std::integral_constant<int, s_>{}, (decltype(U)::value + 1) & 1);
+                stamp(t_st);
                 if (!wconst) load_w(w_cc);
                 load(std::integral_constant<int, s_>{});
+                stamp(t_ld);
             }
             __syncthreads();
+            stamp(t_br);
             return g + 1 < total;
         };
         for (int gi = 0; gi < total; gi += UF) {
@@ -408,6 +425,13 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 if (!iter(S4, gi + 4)) break;
                 if (!iter(S5, gi + 5)) break;
             }
+        }
+        if (DG && p.dbg && lane == 0) {
+            unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + 4 + wid) * 4;
+            d[0] = t_st;
+            d[1] = t_ld;
+            d[2] = t_br;
+            d[3] = __builtin_amdgcn_s_memtime() - t_all;
         }
         __syncthreads();  // stats reduction barrier (MFMA waves)
         return;
@@ -434,9 +458,12 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
     f32x16 acc[RT][NT];
 
+    constexpr bool DG = (WG_EXP & 1024) != 0;
+    unsigned long long t_cp = 0, t_ep = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     int cc = 0, item = 0;
     for (int gi = 0; gi < total; ++gi) {
+        if (DG) t0 = __builtin_amdgcn_s_memtime();
         if (cc == 0) {
 #pragma unroll
             for (int i = 0; i < RT; ++i)
@@ -484,6 +511,11 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         }
         }
 
+        if (DG) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_cp += t1 - t0;
+            t0 = t1;
+        }
         if (++cc == nchunks) {
             // ---------------------------------------------------- epilogue of `item`
             const int sp = slot + item * p.gper;
@@ -564,8 +596,21 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             }
             cc = 0;
             ++item;
+            if (DG) {
+                const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+                t_ep += t1 - t0;
+                t0 = t1;
+            }
         }
         __syncthreads();
+        if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+    }
+    if (DG && p.dbg && lane == 0) {
+        unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + wid) * 4;
+        d[0] = t_cp;
+        d[1] = t_ep;
+        d[2] = t_br;
+        d[3] = __builtin_amdgcn_s_memtime() - t_all;
     }
 
     // ---------------------------------------------------------------- BN statistics row
@@ -1138,6 +1183,13 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
 }  // namespace
 
 // ---------------------------------------------------------------------- host side
+// diagnostics: per-wave cycle counters of timing builds (WG_EXP & 1024) go to this device buffer
+static unsigned long long* g_wg_dbg = nullptr;
+extern "C" int sd_debug_buffer(void* p) {
+    g_wg_dbg = (unsigned long long*)p;
+    return 0;
+}
+
 bool sd_halo_fwd_shape(int N) { return N == 32 || N % 64 == 0; }
 bool sd_halo_fwd_ok(const sd_src& a, int N, int epi) {
     return a.taps == 9 && !a.pool && sd_halo_fwd_shape(N) && epi != SD_EPI_PIXSHUF;
@@ -1286,6 +1338,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.n_split = n_split;
     p.stats = stats;
     p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
+    p.dbg = g_wg_dbg;
     SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= halo_px_cap(t.rt, t.ck) && t.th * t.tw <= 128 * t.rt &&
                    !(st_ && t.rt == 4 && t.ck == 16),
                "sd_conv_gemm(halo): tile %dx%d (RT %d, CK %d)", t.th, t.tw, t.rt, t.ck);
@@ -1337,12 +1390,6 @@ static HTile wgrad_tile(int H, int W) {
     return best;
 }
 
-// diagnostics: per-wave cycle counters of timing builds (WG_EXP & 1024) go to this device buffer
-static unsigned long long* g_wg_dbg = nullptr;
-extern "C" int sd_debug_buffer(void* p) {
-    g_wg_dbg = (unsigned long long*)p;
-    return 0;
-}
 
 // warp-specialised wgrad (k_halo_wgrad_ws): dy channels per block COUT = 64 (M % 64 == 0) or 32 (M == 32),
 // x channels per block CIB = 64 or 32 (the channel count and the first source's width divisible by it;

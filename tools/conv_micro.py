@@ -66,6 +66,17 @@ def run(B, H, W, ci, co, stats, s, dev, n=20):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1000 / n
     name = L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, B, H, W, co, epi)
+    if os.environ.get("SD_WG_DIAG"):  # per-wave cycle counters of a -DWG_EXP=1024 build
+        dbg = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device=dev)
+        L.call("sd_debug_buffer", dbg.data_ptr())
+        once()
+        torch.cuda.synchronize()
+        L.call("sd_debug_buffer", None)
+        d = dbg.view(-1, 8, 4).double().cpu()
+        used = d[:, 0, 3] > 0
+        m, ld = d[used, :4].mean((0, 1)), d[used, 4:].mean((0, 1))
+        print(f"  diag {H}x{W} {ci}->{co}: mfma compute {m[0]:.0f} epilogue {m[1]:.0f} barrier {m[2]:.0f} total {m[3]:.0f}"
+              f" | loader store {ld[0]:.0f} load {ld[1]:.0f} barrier {ld[2]:.0f} total {ld[3]:.0f}", flush=True)
     tot = st.view(rows, co, 2).double().sum(0) if stats else None
     return us, name, o.float(), tot
 
