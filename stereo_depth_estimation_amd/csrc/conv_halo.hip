@@ -20,7 +20,7 @@ namespace {
 constexpr int CK = 32;                           // channels per chunk
 #ifndef WG_EXP
 #define WG_EXP 0  // timing experiments only. wgrad<64>: bit 0 no MFMA phase, 1 no tile loads after the first,
-                  // 2 no LDS stores; halo conv: bit 3 no MFMA phase, 4 no halo loads after the first item, 5 no halo LDS
+                  // 2 no LDS stores; halo conv: bit 3 no MFMA phase, 5 no halo LDS stores, 12 no epilogue stores
                   // stores; k_halo_wgrad_ws: bit 6 no MFMA phase, 7 no LDS stores, 8 no loads and no stores
 #endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -137,6 +137,21 @@ __device__ __forceinline__ uint4 halo_finish_pk(const HaloCol& hc, bool ok, uint
     return ok ? v : make_uint4(0, 0, 0, 0);
 }
 
+// halo_finish_pk's transform on an explicit per-channel affine (8 channels: s0|s1 scales, h0|h1 shifts)
+__device__ __forceinline__ uint4 bnrelu_pk(uint4 raw, float4 s0, float4 s1, float4 h0, float4 h1) {
+    const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
+    const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    unsigned o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float lo = __builtin_fmaf(__uint_as_float(w[i] << 16), s[2 * i], h[2 * i]);
+        const float hi = __builtin_fmaf(__uint_as_float(w[i] & 0xffff0000u), s[2 * i + 1], h[2 * i + 1]);
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2\n\tv_pk_max_i16 %0, %0, 0" : "=v"(o[i]) : "v"(lo), "v"(hi));
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // Partner value for the BN-statistics reduce-scatter level o (16, 8, 4, 2, 1) within each 32-lane
 // half: lanes l and partner(l) differ in bit o and agree above it, which is all the reduce-scatter
 // needs. The partners are chosen to be cheap: lane ^ 16 by ds_swizzle (bit-mask mode, no address
@@ -196,6 +211,7 @@ struct HFwdArgs {
 };
 
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
+constexpr int SBN_MAX = 1024;                       // input channels of the forward/dgrad kernel (LDS BN affine)
 constexpr int HMAX = 384;                           // wgrad halo pixels (>= 17 x 22 for a whole 15x20 image)
 // halo pixels per LDS buffer: 384 (RT 2, and RT 3 at CK 32: 17 x 22 for a whole 15x20 image), 512, 640
 __host__ __device__ constexpr int halo_px_cap(int RT, int CK) { return RT == 4 ? 640 : (RT == 3 && CK == 16 ? 512 : 384); }
@@ -213,7 +229,7 @@ __device__ __forceinline__ int ld_pixel(int item) { return (item / (8 * PPX)) * 
 template <int PPX>
 __device__ __forceinline__ int ld_piece(int item) { return (item >> 3) % PPX; }
 
-template <int NT, int RT, int CK, bool STATS>
+template <int NT, int RT, int CK, bool STATS, bool WCONST>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     constexpr int BN = 32 * NT;
     constexpr int PPX = CK / 8;                          // 16-B pieces per pixel (and per tap of a weight row)
@@ -238,54 +254,94 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     const int bid = p.xcd ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
     const int nb = bid % p.nblk, slot = bid / p.nblk;
     const int n0 = nb * BN;
-    const int nchunks = (p.a.ctot + CK - 1) / CK;
+    // chunks never straddle the two sources (a source's last chunk may be partial): every chunk has one
+    // source, one channel stride and one BN affine
+    const int nc0 = (p.a.c0 + CK - 1) / CK;
+    const int nchunks = nc0 + (p.a.c1 + CK - 1) / CK;
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = my_items * nchunks;            // chunk iterations (block-uniform)
 
+    // the BN affine of every input channel (identity for raw sources), read by the loaders per chunk from LDS
+    __shared__ __attribute__((aligned(16))) float sbn[2 * SBN_MAX + 2 * CK];  // + the tail of a partial chunk
+    for (int c = tid; c < p.a.ctot; c += 512) {
+        const bool first = c < p.a.c0;
+        const int cl = first ? c : c - p.a.c0;
+        const bool bn = (first ? p.a.x0 : p.a.x1) == SD_BNRELU;
+        sbn[c] = bn ? (first ? p.a.sc0 : p.a.sc1)[cl] : 1.f;
+        sbn[SBN_MAX + c] = bn ? (first ? p.a.sh0 : p.a.sh1)[cl] : 0.f;
+    }
+    __syncthreads();
+
     if (is_loader) {
         // =========================================================== loader waves
+        // Per-chunk work is kept to the loads and LDS stores themselves (the loader VALU count per chunk, not
+        // the memory system, bounded the deep layers: ~450 VALU per chunk with per-piece 64-bit address math
+        // and zero-selects). Offsets are 32-bit and precomputed: weights once per block (a chunk adds a scalar
+        // soffset), halo pixels once per item; loads are buffer loads whose out-of-range offset (OOB) returns
+        // zeros without memory traffic, so invalid pieces need no select unless the BN transform follows.
         const int ltid = wid * 64 + lane;
-        int hpix[HP];
-        bool hin[HP];
+        constexpr unsigned OOB = 0x80000000u;
+        const int hw_img = p.H * p.W;
+        const int lpiece = ld_piece<PPX>(ltid);  // this thread's 8-channel piece of every halo pixel
+        unsigned pgeo[HP];                       // (halo row << 16 | halo col) of each piece, ~0 past the halo
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+            const int px = ld_pixel<PPX>(ltid + i * 256);
+            const int hy = px / p.hw;
+            pgeo[i] = px < p.nhalo ? ((unsigned)hy << 16) | (unsigned)(px - hy * p.hw) : 0xffffffffu;
+        }
+        int hpx[HP];  // image-local pixel of each piece for item ld_item, -1 outside the image
+        const __bf16* ib0 = p.a.p0;  // the item's image in source 0 / source 1
+        const __bf16* ib1 = p.a.p1;
         int ld_item = 0, ld_cc = 0;
-        auto geometry = [&]() __attribute__((always_inline)) {  // halo pieces of this thread for item ld_item (chunk-independent)
+        auto geometry = [&]() __attribute__((always_inline)) {
+            // past the block's last item (unconditional loads): every piece out of range, no traffic
+            const bool live = ld_item < my_items;
             const int sp = slot + ld_item * p.gper;
             const int b = sp / p.tiles, tl = sp - b * p.tiles;
             const int ty = tl / p.tiles_x;
-            const int h0 = ty * p.th, w0 = (tl - ty * p.tiles_x) * p.tw;
+            const int h0 = ty * p.th - 1, w0 = (tl - ty * p.tiles_x) * p.tw - 1;
+            ib0 = p.a.p0 + (size_t)b * hw_img * p.a.c0;
+            ib1 = p.a.c1 ? p.a.p1 + (size_t)b * hw_img * p.a.c1 : p.a.p0;
 #pragma unroll
             for (int i = 0; i < HP; ++i) {
-                const int px = ld_pixel<PPX>(ltid + i * 256);
-                const int hy = px / p.hw, hxx = px - hy * p.hw;
-                const int h = h0 - 1 + hy, w = w0 - 1 + hxx;
-                hin[i] = (px < p.nhalo) & (h >= 0) & (w >= 0) & (h < p.H) & (w < p.W);
-                hpix[i] = hin[i] ? (b * p.H + h) * p.W + w : 0;
+                const int h = h0 + (int)(pgeo[i] >> 16), w = w0 + (int)(pgeo[i] & 0xffffu);
+                const bool in = live & (pgeo[i] != 0xffffffffu) & (h >= 0) & (w >= 0) & (h < p.H) & (w < p.W);
+                hpx[i] = in ? h * p.W + w : -1;
             }
         };
-        // Two halo register sets: chunk j is staged in set j&1 between its load and its store, so the
-        // halo loads of TWO chunks are in flight while the MFMA waves compute a third (with one chunk
-        // of cover the iteration waited on a whole memory round trip at the HBM-bound layers). The
-        // weights (L2-resident) take one set, loaded one chunk ahead: right after the previous
-        // chunk's weights are stored.
-        // Loads are unconditional (chunks past the end re-read valid addresses and are never
-        // stored), which keeps the in-order vmcnt bookkeeping static: each store waits only for
-        // its own set.
-        // LS register sets: chunk j lives in set j % LS between its load and its store, so up to LS chunks'
-        // halo loads are in flight while the MFMA waves compute another.
-        // UNCOND: the N = 32 instances (full resolution, HBM-bound) keep their loads unconditional so vmcnt stays
-        // countable and every set's loads stay in flight until its store; that gives the 8-channel input 3
-        // sets' cover at LS = 4 and made LS = 3 spill, so LS = 2 there. The N % 64 instances measured 2-5 %
-        // slower with unconditional loads (more requests in flight beside the MFMA-bound body) and keep the
-        // guarded form.
-        constexpr bool UNCOND = NT == 1;
+        // weights: byte offset of each piece in chunk 0 (OOB: past the weight rows of this N-block)
+        const __amdgpu_buffer_rsrc_t wrs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)p.wp, (short)0, p.N * p.kpad * 2, 0x00020000);
+        unsigned woff[W_PER_THREAD];
+#pragma unroll
+        for (int i = 0; i < W_PER_THREAD; ++i) {
+            const int item = ltid + i * 256;
+            const int co = item / (9 * PPX), r = item - co * (9 * PPX), tap = r / PPX, sp = r - tap * PPX;
+            woff[i] = ((item < WPIECES) & (n0 + co < p.N)) ? (unsigned)((n0 + co) * p.kpad + tap * p.a.ctot + sp * 8) * 2u
+                                                          : OOB;
+            asm volatile("" : "+v"(woff[i]));  // kept in registers, not recomputed per chunk
+        }
+        // Software pipeline, one iteration per chunk g: store chunk g (set g % LS, loaded LS iterations ago) and
+        // the weights of chunk g (loaded one iteration ago) into LDS buffer g & 1, load the weights of chunk g+1
+        // and the halo of chunk g+LS, barrier; the MFMA waves compute chunk g-1 meanwhile. Every iteration
+        // issues the same loads and waits on every path (chunks past the block's last are out of range, no
+        // traffic): a load or a wait on only some paths, or a prologue whose loads differ from an iteration's,
+        // makes the compiler's vmcnt bookkeeping merge pessimistically; it then drained every outstanding load
+        // before the next loads and left one chunk of latency cover instead of LS. VMEM loads complete in
+        // order, so waiting for the weights of chunk g also waits for everything issued before them: they are
+        // issued after the halo of chunk g+LS-1 and before that of chunk g+LS.
+        // LS register sets: up to LS chunks' halo loads are in flight while the MFMA waves compute another
+        // (the 8-channel input, one chunk per item, no weight loads in the loop: LS = 4).
         constexpr int LS = NT == 1 && CK == 8 ? 4 : 2;
-        constexpr int UF = LS == 3 ? 6 : LS;  // unroll: both the set (j % LS) and the buffer (j & 1) static
+        static_assert(LS == 2 || LS == 4, "set (g % LS) and buffer (g & 1) static per unrolled iteration");
         // one object per set (an array of sets past ~256 B stays in scratch instead of registers)
         struct HSet {
             uint4 hr[HP];
-            unsigned m;  // bit i: piece i valid (else stored as zeros)
-            HaloCol hc;
+            unsigned m;  // bit i: piece i inside the image (and the channels)
+            int cb;      // the chunk's first channel (BN affine index)
+            bool bn;     // BN+ReLU source
         };
         HSet st0, st1, st2, st3;
         auto set_of = [&](auto S) __attribute__((always_inline)) -> HSet& {
@@ -295,22 +351,29 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             else return st3;
         };
         uint4 wr[W_PER_THREAD];
-        unsigned wokm;
-        // one chunk per item: the weights are the same for every item of this block (fixed N-block),
+        // WCONST (one chunk per item): the weights are the same for every item of this block (fixed N-block),
         // so they are loaded once and stored into both LDS buffers in the prologue
-        const bool wconst = nchunks == 1;
-        int w_cc = 0;  // chunk (within the item) of the weights in wr
-        auto load_w = [&](int cc) __attribute__((always_inline)) {
-            wokm = 0;
+        int w_cc = 0;  // chunk (within the item) of the next weights to load
+        auto load_w = [&]() __attribute__((always_inline)) {  // weights of chunk w_cc -> wr, then advance
+            const bool s1 = w_cc >= nc0;
+            const int C = s1 ? p.a.c1 : p.a.c0;
+            const int cl = (s1 ? w_cc - nc0 : w_cc) * CK;
+            if (++w_cc == nchunks) w_cc = 0;
+            unsigned v[W_PER_THREAD];
+#pragma unroll
+            for (int i = 0; i < W_PER_THREAD; ++i) v[i] = woff[i];
+            if (cl + CK > C) {  // partial chunk: pieces past the source's channels read zeros
+#pragma unroll
+                for (int i = 0; i < W_PER_THREAD; ++i) {
+                    const int sp = ((ltid + i * 256) % (9 * PPX)) % PPX;
+                    if (cl + sp * 8 >= C) v[i] = OOB;
+                }
+            }
+            const int cbg = (s1 ? p.a.c0 : 0) + cl;  // first channel of the chunk in the packed k = tap*ctot + c
 #pragma unroll
             for (int i = 0; i < W_PER_THREAD; ++i) {
-                const int item = ltid + i * 256;
-                const int co = item / (9 * PPX), r = item - co * (9 * PPX), tap = r / PPX, sp = r - tap * PPX;
-                const int c = cc * CK + sp * 8;
-                const bool ok = (item < WPIECES) & (c < p.a.ctot) & (n0 + co < p.N);
-                wokm |= (unsigned)ok << i;
-                // raw load; the zero-select happens at store time (selecting here would wait for the load)
-                wr[i] = *reinterpret_cast<const uint4*>(p.wp + (ok ? (size_t)(n0 + co) * p.kpad + tap * p.a.ctot + c : 0));
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(wrs, v[i], cbg * 2, 0);
+                wr[i] = make_uint4(x[0], x[1], x[2], x[3]);
             }
         };
         auto store_w = [&](int buf) __attribute__((always_inline)) {
@@ -319,71 +382,68 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             for (int i = 0; i < W_PER_THREAD; ++i) {
                 const int item = ltid + i * 256;
                 const int co = item / (9 * PPX), r = item - co * (9 * PPX);
-                if (item < WPIECES)
-                    *reinterpret_cast<uint4*>(wl + co * W_LD + r * 8) = ((wokm >> i) & 1u) ? wr[i] : make_uint4(0, 0, 0, 0);
+                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * W_LD + r * 8) = wr[i];
             }
         };
         auto load = [&](auto S) __attribute__((always_inline)) {  // halo of chunk (ld_item, ld_cc) -> register set S, then advance
-            const int cc = ld_cc;
             HSet& q = set_of(S);
-            q.hc = halo_col(p.a, cc * CK + ld_piece<PPX>(ltid) * 8, p.wp);
+            const bool s1 = ld_cc >= nc0;
+            const int C = s1 ? p.a.c1 : p.a.c0;
+            const int cl = (s1 ? ld_cc - nc0 : ld_cc) * CK;
+            q.cb = (s1 ? p.a.c0 : 0) + cl;
+            q.bn = (s1 ? p.a.x1 : p.a.x0) == SD_BNRELU;
+            const bool cok = cl + lpiece * 8 < C;
+            // one buffer load per piece on the source's image; pieces outside the image or past the source's
+            // channels are out of range (zeros; masked again after a BN transform)
+            const __amdgpu_buffer_rsrc_t hrs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(s1 ? ib1 : ib0), (short)0, hw_img * C * 2, 0x00020000);
             unsigned m = 0;
 #pragma unroll
             for (int i = 0; i < HP; ++i) {
-                const bool ok = hin[i] & q.hc.cok;
+                const bool ok = (hpx[i] >= 0) & cok;
                 m |= (unsigned)ok << i;
-                if (!(WG_EXP & 16) || ld_item == 0)
-                    q.hr[i] = *reinterpret_cast<const uint4*>(q.hc.base + (ok ? (size_t)hpix[i] * q.hc.C + q.hc.c : 0));
+                unsigned off;
+                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(hpx[i]), "s"(C * 2), "v"(lpiece * 16));
+                off = ok ? off : OOB;
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(hrs, off, cl * 2, 0);
+                q.hr[i] = make_uint4(x[0], x[1], x[2], x[3]);
             }
             q.m = m;
             if (++ld_cc == nchunks) {
                 ld_cc = 0;
                 ++ld_item;
-                if (ld_item < my_items) geometry();
+                geometry();
             }
         };
         auto store = [&](auto S, int buf) __attribute__((always_inline)) {  // halo set S and the weights in wr -> LDS buffer buf
+            HSet& q = set_of(S);
             __bf16* hx = smem + buf * BUF;
+            float4 s0, s1, h0, h1;
+            if (q.bn) {
+                const float* sc = sbn + q.cb + lpiece * 8;
+                s0 = *reinterpret_cast<const float4*>(sc);
+                s1 = *reinterpret_cast<const float4*>(sc + 4);
+                h0 = *reinterpret_cast<const float4*>(sc + SBN_MAX);
+                h1 = *reinterpret_cast<const float4*>(sc + SBN_MAX + 4);
+            }
             if (!(WG_EXP & 32))
 #pragma unroll
             for (int i = 0; i < HP; ++i) {  // every piece lands inside the halo region
                 const int item = ltid + i * 256;
-                *reinterpret_cast<uint4*>(hx + ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8) =
-                    halo_finish_pk(set_of(S).hc, (set_of(S).m >> i) & 1u, set_of(S).hr[i]);
+                uint4 v = q.hr[i];
+                const bool ok = (q.m >> i) & 1u;
+                if (q.bn) {
+                    v = bnrelu_pk(v, s0, s1, h0, h1);
+                    v = ok ? v : make_uint4(0, 0, 0, 0);  // zero padding after the activation
+                }
+                *reinterpret_cast<uint4*>(hx + ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8) = v;
             }
-            if (!wconst) {
-                store_w(buf);
-                if (++w_cc == nchunks) w_cc = 0;
-            }
+            if constexpr (!WCONST) store_w(buf);
         };
         constexpr std::integral_constant<int, 0> S0{};
         constexpr std::integral_constant<int, 1> S1{};
         constexpr std::integral_constant<int, 2> S2{};
         constexpr std::integral_constant<int, 3> S3{};
-        constexpr std::integral_constant<int, 4> S4{};
-        constexpr std::integral_constant<int, 5> S5{};
-        if (total > 0) {
-            geometry();
-            load_w(0);
-            if (wconst) {
-                store_w(0);
-                store_w(1);
-            }
-            load(S0);  // chunks 0 .. LS-1
-            load(S1);
-            if constexpr (LS >= 3) load(S2);
-            if constexpr (LS >= 4) load(S3);
-            store(S0, 0);
-            if (!wconst) load_w(w_cc);  // chunk 1's weights
-            load(S0);  // chunk LS
-        }
-        __syncthreads();
-        // iteration g: the MFMA waves read buffer g&1; store chunk g+1 (set (g+1) % LS) into the other
-        // buffer and refill that set with chunk g+1+LS. Unrolled by LS so set and buffer indices are
-        // static; returns false after the last iteration's barrier.
-        // The loads are unconditional (past the last chunk they re-read valid addresses and are never stored):
-        // a load issued on only some paths makes the compiler's vmcnt bookkeeping drain every outstanding load
-        // before each store, which left one chunk of latency cover instead of LS
         constexpr bool DG = (WG_EXP & 1024) != 0;
         unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
         auto stamp = [&](unsigned long long& acc_) __attribute__((always_inline)) {
@@ -394,36 +454,44 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 t0 = t1;
             }
         };
-        auto iter = [&](auto U, int g) __attribute__((always_inline)) {
-            constexpr int s_ = (decltype(U)::value + 1) % LS;
+        auto iter = [&](auto U) __attribute__((always_inline)) {
             if (DG) t0 = __builtin_amdgcn_s_memtime();
-            if constexpr (UNCOND) {
-                if (g + 1 < total) store(std::integral_constant<int, s_>{}, (decltype(U)::value + 1) & 1);
-                stamp(t_st);
-                if (!wconst) load_w(w_cc);
-                load(std::integral_constant<int, s_>{});
-                stamp(t_ld);
-            } else if (g + 1 < total) {
-                store(std::integral_constant<int, s_>{}, (decltype(U)::value + 1) & 1);
-                stamp(t_st);
-                if (!wconst) load_w(w_cc);
-                load(std::integral_constant<int, s_>{});
-                stamp(t_ld);
-            }
+            store(U, decltype(U)::value & 1);
+            stamp(t_st);
+            if constexpr (!WCONST) load_w();
+            load(U);
+            stamp(t_ld);
             __syncthreads();
             stamp(t_br);
-            return g + 1 < total;
         };
-        for (int gi = 0; gi < total; gi += UF) {
-            if (!iter(S0, gi)) break;
-            if (!iter(S1, gi + 1)) break;
-            if constexpr (UF >= 4) {
-                if (!iter(S2, gi + 2)) break;
-                if (!iter(S3, gi + 3)) break;
+        if (total > 0) {
+            // the loads an iteration would have issued before chunk 0: the halo of chunks 0 .. LS-2, the weights
+            // of chunk 0, the halo of chunk LS-1 (WCONST: the weights first, stored right away)
+            geometry();
+            if constexpr (WCONST) {
+                load_w();
+                store_w(0);
+                store_w(1);
             }
-            if constexpr (UF == 6) {
-                if (!iter(S4, gi + 4)) break;
-                if (!iter(S5, gi + 5)) break;
+            load(S0);
+            if constexpr (LS == 4) {
+                load(S1);
+                load(S2);
+            }
+            if constexpr (!WCONST) load_w();
+            if constexpr (LS == 4) load(S3);
+            else load(S1);
+            for (int gi = 0;; gi += LS) {
+                iter(S0);
+                if (gi + 1 >= total) break;
+                iter(S1);
+                if (gi + 2 >= total) break;
+                if constexpr (LS == 4) {
+                    iter(S2);
+                    if (gi + 3 >= total) break;
+                    iter(S3);
+                    if (gi + 4 >= total) break;
+                }
             }
         }
         if (DG && p.dbg && lane == 0) {
@@ -460,10 +528,15 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 
     constexpr bool DG = (WG_EXP & 1024) != 0;
     unsigned long long t_cp = 0, t_ep = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
-    __syncthreads();
     int cc = 0, item = 0;
     for (int gi = 0; gi < total; ++gi) {
         if (DG) t0 = __builtin_amdgcn_s_memtime();
+        __syncthreads();  // chunk gi is in buffer gi & 1 (and the loaders may overwrite the other one)
+        if (DG) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_br += t1 - t0;
+            t0 = t1;
+        }
         if (cc == 0) {
 #pragma unroll
             for (int i = 0; i < RT; ++i)
@@ -567,7 +640,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                         const auto ry = __builtin_amdgcn_permlane32_swap(pk[k].y, pk[k + 1].y, false, false);
                         const uint4 o = make_uint4(rx[0], ry[0], rx[1], ry[1]);
                         const int c = n0 + t * 32 + 8 * k + 2 * chq;  // lane >= 32: group k+1
-                        if (!ok || c >= p.N) continue;
+                        if (!ok || c >= p.N || (WG_EXP & 4096)) continue;
                         __bf16* dst;
                         if (!STATS && p.epi == SD_EPI_SPLIT)  // STATS launches never split (fewer live registers)
                             dst = c < p.n_split ? p.out0 + pix * p.n_split + c
@@ -602,8 +675,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 t0 = t1;
             }
         }
-        __syncthreads();
-        if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
     }
     if (DG && p.dbg && lane == 0) {
         unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + wid) * 4;
@@ -1192,7 +1263,8 @@ extern "C" int sd_debug_buffer(void* p) {
 
 bool sd_halo_fwd_shape(int N) { return N == 32 || N % 64 == 0; }
 bool sd_halo_fwd_ok(const sd_src& a, int N, int epi) {
-    return a.taps == 9 && !a.pool && sd_halo_fwd_shape(N) && epi != SD_EPI_PIXSHUF;
+    return a.taps == 9 && !a.pool && sd_halo_fwd_shape(N) && epi != SD_EPI_PIXSHUF &&
+           a.chans[0] + a.chans[1] <= SBN_MAX;
 }
 
 // XCD-contiguous block numbering in the halo kernels (SD_HALO_XCD=0: hardware order, for A/B runs)
@@ -1306,12 +1378,19 @@ const char* sd_halo_fwd_name(int H, int W, int N, int epi, int ctot) {
     return buf;
 }
 
+// wconst (one chunk per item): the weights are staged once per block. CK = 8 always has one chunk; CK = 16
+// (experiments) always takes the general instance, which is also correct with one chunk.
 template <int NT, int RT, int CK>
-static void launch_halo(bool stats, dim3 grid, hipStream_t st, const HFwdArgs& p) {
-    if (stats)
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true>), grid, dim3(512), 0, st, p);
+static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p) {
+    constexpr bool W0 = CK == 8, W1 = CK != 16;  // the instance for wconst false / true
+    if (stats && (wconst ? W1 : W0))
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W1>), grid, dim3(512), 0, st, p);
+    else if (stats)
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W0>), grid, dim3(512), 0, st, p);
+    else if (wconst ? W1 : W0)
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1>), grid, dim3(512), 0, st, p);
     else
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0>), grid, dim3(512), 0, st, p);
 }
 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
@@ -1343,24 +1422,30 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
                    !(st_ && t.rt == 4 && t.ck == 16),
                "sd_conv_gemm(halo): tile %dx%d (RT %d, CK %d)", t.th, t.tw, t.rt, t.ck);
     SD_REQUIRE((long long)batch * p.tiles < (1LL << 30), "sd_conv_gemm(halo): too many tiles");
+    // 32-bit buffer offsets: image-local halo offsets (24-bit pixel index) and the packed weights
+    SD_REQUIRE((long long)H * W < (1LL << 24) && (long long)H * W * (a.chans[0] > a.chans[1] ? a.chans[0] : a.chans[1]) * 2 <
+                   (1LL << 31) && (long long)N * kpad * 2 < (1LL << 31),
+               "sd_conv_gemm(halo): image %dx%d or weights %dx%d too large for 32-bit offsets", H, W, N, kpad);
     const dim3 grid(p.gper * p.nblk);
+    const bool wc = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck) == 1;
+    SD_REQUIRE(t.ck != 8 || wc, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
     if (t.ck == 8) {
-        if (t.rt == 4) launch_halo<1, 4, 8>(st_, grid, st, p);
-        else if (t.rt == 3) launch_halo<1, 3, 8>(st_, grid, st, p);
-        else launch_halo<1, 2, 8>(st_, grid, st, p);
+        if (t.rt == 4) launch_halo<1, 4, 8>(st_, wc, grid, st, p);
+        else if (t.rt == 3) launch_halo<1, 3, 8>(st_, wc, grid, st, p);
+        else launch_halo<1, 2, 8>(st_, wc, grid, st, p);
     } else if (N == 32) {
-        if (t.rt == 4) launch_halo<1, 4, 32>(st_, grid, st, p);
-        else if (t.rt == 3) launch_halo<1, 3, 32>(st_, grid, st, p);
-        else launch_halo<1, 2, 32>(st_, grid, st, p);
+        if (t.rt == 4) launch_halo<1, 4, 32>(st_, wc, grid, st, p);
+        else if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p);
+        else launch_halo<1, 2, 32>(st_, wc, grid, st, p);
     } else if (t.ck == 32) {
-        if (t.rt == 3) launch_halo<2, 3, 32>(st_, grid, st, p);
-        else launch_halo<2, 2, 32>(st_, grid, st, p);
+        if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p);
+        else launch_halo<2, 2, 32>(st_, wc, grid, st, p);
     } else if (t.rt == 4) {
-        hipLaunchKernelGGL((k_halo_conv<2, 4, 16, false>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<2, 4, 16, false, false>), grid, dim3(512), 0, st, p);
     } else if (t.rt == 3) {
-        launch_halo<2, 3, 16>(st_, grid, st, p);
+        launch_halo<2, 3, 16>(st_, wc, grid, st, p);
     } else {
-        launch_halo<2, 2, 16>(st_, grid, st, p);
+        launch_halo<2, 2, 16>(st_, wc, grid, st, p);
     }
     return sd_check_launch("sd_conv_gemm(halo)");
 }
