@@ -241,7 +241,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     constexpr int HALO_ELEMS = HP * 256 / PPX * HX_LD, W_ELEMS = BN * W_LD, BUF = HALO_ELEMS + W_ELEMS;
     constexpr int KS = (9 * CK + 15) / 16;               // 16-deep k-steps per chunk (CK 8: 5, the last half padding)
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
-    __shared__ float redf[4 * BN * 2];
+    // epilogue transpose scratch: 32 pixels x BN channels per MFMA wave (its own region, no block sync)
+    __shared__ __attribute__((aligned(16))) __bf16 scr[4 * 32 * BN];
 
     // waves 0-3 land on the 4 different SIMDs (dispatch order 0->2->1->3, measured), and so do 4-7:
     // one MFMA wave and one loader wave per SIMD
@@ -272,6 +273,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         sbn[SBN_MAX + c] = bn ? (first ? p.a.sh0 : p.a.sh1)[cl] : 0.f;
     }
     __syncthreads();
+    float* const redf = sbn;  // [4][BN][2] BN statistics after the last item (the loaders no longer read sbn)
+    static_assert(4 * BN * 2 <= 2 * SBN_MAX, "redf fits in sbn");
 
     if (is_loader) {
         // =========================================================== loader waves
@@ -452,6 +455,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 const unsigned long long t1 = __builtin_amdgcn_s_memtime();
                 acc_ += t1 - t0;
                 t0 = t1;
+            } else if (WG_EXP & 8192) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         };
         auto iter = [&](auto U) __attribute__((always_inline)) {
@@ -515,27 +520,58 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         const int hm = m / p.tw, wm = m - hm * p.tw;
         abase[i] = m < mvalid ? hm * p.hw + wm : 0;
     }
-    // BN statistics of the stored values. Each item's 32*NT per-lane (sum, sumsq) values are
-    // reduce-scattered over the 32 lanes that share channels (lane bits 0-4), so a lane keeps only NT
-    // running values across the block's items instead of 32*NT registers
-    // (NT = 2). NT = 1 keeps the plain per-lane accumulators (32 registers, reduced once at the end).
-    constexpr bool RS = NT == 2;
-    constexpr int NOWN = !STATS ? 1 : (RS ? NT : 32);
-    float own[NOWN];  // RS: [j] = k = NT*(lane & 31) + j;  else: [(r)*2 + kind] for the lane's 16 channels
+    // BN statistics of the stored values, taken from the transposed pieces: a lane always reads channels
+    // n0 + 8*(lane % PPP) + 0..7, so it keeps 8 (sum, sumsq) pairs across all of the block's items and the
+    // lanes sharing channels are reduced once at the end.
+    constexpr int NOWN = STATS ? 16 : 1;
+    float own[NOWN];  // [q*2 + {sum, sumsq}] of channel n0 + 8*(lane % PPP) + q
 #pragma unroll
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
     f32x16 acc[RT][NT];
+    // Epilogue: the bf16 results go through this wave's LDS scratch (pixel rows of BN channels, 16-B pieces
+    // XOR-swizzled by pixel so both the row-per-lane writes and the piece-per-lane reads are conflict-free)
+    // and leave as stores of EPR whole pixels per instruction (1 KiB contiguous, 8 or 16 full 128-B lines)
+    // instead of 32 pixels x 32 B: the scattered form made the MFMA waves wait on store issue for ~20 % of
+    // the kernel at full resolution. Buffer stores: pixels outside the image are out of range (dropped).
+    constexpr int PPP = NT * 4;      // 16-B pieces per pixel row
+    constexpr int EPR = 64 / PPP;    // pixels per store instruction
+    constexpr int ER = 32 / EPR;     // store instructions per 32-pixel tile
+    auto swz = [](int j, int px) { return NT == 2 ? j ^ (px & 7) : j ^ ((px >> 1) & 3); };
+    // tile-relative (row << 9 | col) of the pixel this lane stores, 0xffff past the tile; two per register
+    // (tiles are < 64 rows and < 512 columns, halo_tile)
+    unsigned erel[(RT * ER + 1) / 2];
+#pragma unroll
+    for (int k = 0; k < (RT * ER + 1) / 2; ++k) erel[k] = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int r = 0; r < ER; ++r) {
+            const int m = (wid + 4 * i) * 32 + r * EPR + lane / PPP;
+            const int hm = m / p.tw, wm = m - hm * p.tw;
+            const unsigned v = m < mvalid ? (unsigned)((hm << 9) | wm) : 0xffffu;
+            const int k = i * ER + r;
+            erel[k / 2] = (erel[k / 2] & ~(0xffffu << (16 * (k & 1)))) | (v << (16 * (k & 1)));
+        }
+    __bf16* const scw = scr + wid * 32 * BN;
 
     constexpr bool DG = (WG_EXP & 1024) != 0;
     unsigned long long t_cp = 0, t_ep = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
     int cc = 0, item = 0;
     for (int gi = 0; gi < total; ++gi) {
         if (DG) t0 = __builtin_amdgcn_s_memtime();
+        if (WG_EXP & 16384) {
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
         __syncthreads();  // chunk gi is in buffer gi & 1 (and the loaders may overwrite the other one)
         if (DG) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             t_br += t1 - t0;
             t0 = t1;
+        }
+        if (WG_EXP & 16384) {
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (cc == 0) {
 #pragma unroll
@@ -589,23 +625,26 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             t_cp += t1 - t0;
             t0 = t1;
         }
+        if (WG_EXP & 16384) {
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if (++cc == nchunks) {
             // ---------------------------------------------------- epilogue of `item`
             const int sp = slot + item * p.gper;
             const int b = sp / p.tiles, tl = sp - b * p.tiles;
             const int ty = tl / p.tiles_x;
             const int h0 = ty * p.th, w0 = (tl - ty * p.tiles_x) * p.tw;
-            const int chq = 4 * (lane >> 5);  // this lane's channel offset within each 8-channel group
-            constexpr int NSV = STATS && RS ? 32 * NT : 1;
-            float sv[NSV];  // RS: [(t*16 + r)*2 + {sum, sumsq}] over this lane's RT pixels of the item
-#pragma unroll
-            for (int k = 0; k < NSV; ++k) sv[k] = 0.f;
+            const int hw_img = p.H * p.W;
+            const bool split = !STATS && p.epi == SD_EPI_SPLIT;  // STATS launches never split
+            const int ns = split ? p.n_split : p.N;
+            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(p.out0 + (size_t)b * hw_img * ns), (short)0, hw_img * ns * 2, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(split ? p.out1 + (size_t)b * hw_img * (p.N - ns) : p.out0), (short)0,
+                split ? hw_img * (p.N - ns) * 2 : 0, 0x00020000);
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
-                const int m = (wid + 4 * i) * 32 + (lane & 31);
-                const int hm = m / p.tw, wm = m - hm * p.tw;
-                const bool ok = (m < mvalid) & (h0 + hm < p.H) & (w0 + wm < p.W);
-                const size_t pix = ((size_t)b * p.H + h0 + hm) * p.W + w0 + wm;
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
                     uint2 pk[4];  // this lane's 4 channels of each 8-channel group g4, packed bf16
@@ -615,57 +654,52 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[i][t][4 * g4 + q];
                         pk[g4] = *reinterpret_cast<uint2*>(&v);
-                        if constexpr (STATS) {
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const float f = ok ? (float)v[q] : 0.f;
-                                if constexpr (RS) {
-                                    sv[(t * 16 + 4 * g4 + q) * 2] += f;
-                                    sv[(t * 16 + 4 * g4 + q) * 2 + 1] += f * f;
-                                } else {
-                                    own[(4 * g4 + q) * 2] += f;
-                                    own[(4 * g4 + q) * 2 + 1] += f * f;
-                                }
-                            }
-                        }
                     }
-                    // 16-B stores (cdna_hip_programming.md T21): lanes l and l+32 hold the two 4-channel halves
-                    // of each 8-channel group of one pixel. v_permlane32_swap on groups (k, k+1) leaves group k
-                    // whole in lane l and group k+1 whole in lane l+32: 2 dwordx4 stores instead of 4 dwordx2
-                    // (the full-resolution N = 32 layers were store-issue-bound). All lanes take part in the
-                    // swaps; the pixel mask applies to the stores only.
+                    // lanes l and l+32 hold the two 4-channel halves of each 8-channel group of one pixel:
+                    // v_permlane32_swap on groups (k, k+1) leaves group k whole in lane l and group k+1 in l+32
 #pragma unroll
                     for (int k = 0; k < 4; k += 2) {
                         const auto rx = __builtin_amdgcn_permlane32_swap(pk[k].x, pk[k + 1].x, false, false);
                         const auto ry = __builtin_amdgcn_permlane32_swap(pk[k].y, pk[k + 1].y, false, false);
-                        const uint4 o = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-                        const int c = n0 + t * 32 + 8 * k + 2 * chq;  // lane >= 32: group k+1
-                        if (!ok || c >= p.N || (WG_EXP & 4096)) continue;
-                        __bf16* dst;
-                        if (!STATS && p.epi == SD_EPI_SPLIT)  // STATS launches never split (fewer live registers)
-                            dst = c < p.n_split ? p.out0 + pix * p.n_split + c
-                                                : p.out1 + pix * (p.N - p.n_split) + (c - p.n_split);
-                        else
-                            dst = p.out0 + pix * p.N + c;
-                        *reinterpret_cast<uint4*>(dst) = o;
+                        const int px = lane & 31, j = t * 4 + k + (lane >> 5);
+                        *reinterpret_cast<uint4*>(scw + px * BN + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
                     }
                 }
-            }
-            if constexpr (STATS && RS) {
-                // halve the vector at each lane bit o = 16..1: the lane with bit o clear keeps the low half
-                // (plus its partner's low half), the other the high half; k = NT*lane + j at the end
+                asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
 #pragma unroll
-                for (int o = 16, len = 32 * NT; o >= 1; o >>= 1, len >>= 1) {
-                    const bool hi = (lane & o) != 0;
+                for (int r = 0; r < ER; ++r) {
+                    const int px = r * EPR + lane / PPP, j = lane % PPP;
+                    const uint4 v = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
+                    const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
+                    const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
+                    const bool live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
+                    const bool in = live & !(WG_EXP & 4096);
+                    const int pix = h * p.W + w, c = n0 + j * 8;
+                    if constexpr (STATS) {
+                        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                    for (int j = 0; j < len / 2; ++j) {
-                        const float keep = hi ? sv[j + len / 2] : sv[j];
-                        const float send = hi ? sv[j] : sv[j + len / 2];
-                        sv[j] = keep + rs_partner(send, o);
+                        for (int q = 0; q < 4; ++q) {
+                            const float lo = live ? __uint_as_float(wv[q] << 16) : 0.f;
+                            const float hi = live ? __uint_as_float(wv[q] & 0xffff0000u) : 0.f;
+                            own[4 * q] += lo;
+                            own[4 * q + 1] = __builtin_fmaf(lo, lo, own[4 * q + 1]);
+                            own[4 * q + 2] += hi;
+                            own[4 * q + 3] = __builtin_fmaf(hi, hi, own[4 * q + 3]);
+                        }
+                    }
+                    __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
+                    if (!split) {
+                        const unsigned off = (in & (c < p.N)) ? (unsigned)(pix * p.N + c) * 2u : 0x80000000u;
+                        __builtin_amdgcn_raw_buffer_store_b128(data, rs0, off, 0, 0);
+                    } else {  // dgrad of a concatenation: channels < n_split to out0, the rest to out1
+                        const unsigned o0 = (in & (c < ns)) ? (unsigned)(pix * ns + c) * 2u : 0x80000000u;
+                        const unsigned o1 = (in & (c >= ns) & (c < p.N)) ? (unsigned)(pix * (p.N - ns) + c - ns) * 2u
+                                                                       : 0x80000000u;
+                        __builtin_amdgcn_raw_buffer_store_b128(data, rs0, o0, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(data, rs1, o1, 0, 0);
                     }
                 }
-#pragma unroll
-                for (int j = 0; j < NT; ++j) own[j] += sv[j];
+                asm volatile("" ::: "memory");  // the next tile's writes after these reads
             }
             cc = 0;
             ++item;
@@ -685,27 +719,16 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     }
 
     // ---------------------------------------------------------------- BN statistics row
-    if constexpr (STATS && RS) {
-        // lane l owns k = NT*(l & 31) + j of its half's [(t*16 + r)*2 + kind] vector (the highest lane
-        // bit was reduced first and chose the highest index bit)
-#pragma unroll
-        for (int j = 0; j < NOWN; ++j) {
-            const int k = NT * (lane & 31) + j, kind = k & 1, r = (k >> 1) & 15, t = k >> 5;
-            redf[(wid * BN + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 2 + kind] = own[j];
-        }
-    } else if constexpr (STATS) {
-        // lanes sharing lane>>5 hold the same channels for different pixels: butterfly over lane bits 0-4
+    if constexpr (STATS) {
+        // lanes l, l + PPP, l + 2*PPP, ... hold the same 8 channels (of different pixels)
 #pragma unroll
         for (int k = 0; k < NOWN; ++k) {
 #pragma unroll
-            for (int o = 1; o < 32; o <<= 1) own[k] += __shfl_xor(own[k], o);
+            for (int o = PPP; o < 64; o <<= 1) own[k] += __shfl_xor(own[k], o);
         }
-        if ((lane & 31) == 0) {
+        if (lane < PPP) {
 #pragma unroll
-            for (int k = 0; k < NOWN; ++k) {
-                const int r = k >> 1;
-                redf[(wid * BN + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 2 + (k & 1)] = own[k];
-            }
+            for (int k = 0; k < NOWN; ++k) redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] = own[k];
         }
     }
     __syncthreads();
@@ -1315,7 +1338,7 @@ static HTile halo_tile(int H, int W, int N, bool stats) {
         else if (W % 40 == 0)
             t = {6, 40, 0, 32};
         else if (W <= 256) {
-            int th = 256 / W;
+            int th = 256 / W < 63 ? 256 / W : 63;
             while (th > 1 && !fits(th, W)) --th;
             if (fits(th, W)) t = {th, W, 0, 32};
         }
@@ -1329,7 +1352,7 @@ static HTile halo_tile(int H, int W, int N, bool stats) {
     double best_cost = 1e300;
     for (int tw = 1; tw <= (W < 128 ? W : 128); ++tw) {
         if (tw != W && tw != 32 && W % tw) continue;
-        for (int th = 1; th <= H && th * tw <= 128 * rt_max; ++th) {
+        for (int th = 1; th <= H && th < 64 && th * tw <= 128 * rt_max; ++th) {
             int rt = (th * tw + 127) / 128;
             if (rt < 2) rt = 2;
             while (rt <= rt_max && (th + 2) * (tw + 2) > halo_px_cap(rt, 16)) ++rt;
@@ -1419,12 +1442,13 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
     p.dbg = g_wg_dbg;
     SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= halo_px_cap(t.rt, t.ck) && t.th * t.tw <= 128 * t.rt &&
+                   t.th < 64 && t.tw < 512 &&
                    !(st_ && t.rt == 4 && t.ck == 16),
                "sd_conv_gemm(halo): tile %dx%d (RT %d, CK %d)", t.th, t.tw, t.rt, t.ck);
     SD_REQUIRE((long long)batch * p.tiles < (1LL << 30), "sd_conv_gemm(halo): too many tiles");
     // 32-bit buffer offsets: image-local halo offsets (24-bit pixel index) and the packed weights
     SD_REQUIRE((long long)H * W < (1LL << 24) && (long long)H * W * (a.chans[0] > a.chans[1] ? a.chans[0] : a.chans[1]) * 2 <
-                   (1LL << 31) && (long long)N * kpad * 2 < (1LL << 31),
+                   (1LL << 31) && (long long)N * kpad * 2 < (1LL << 31) && (long long)H * W * N * 2 < (1LL << 31),
                "sd_conv_gemm(halo): image %dx%d or weights %dx%d too large for 32-bit offsets", H, W, N, kpad);
     const dim3 grid(p.gper * p.nblk);
     const bool wc = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck) == 1;
