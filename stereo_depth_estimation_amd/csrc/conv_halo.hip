@@ -262,6 +262,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = my_items * nchunks;            // chunk iterations (block-uniform)
+    constexpr int LS = NT == 1 && CK == 8 ? 4 : 2;   // loader register sets (chunks in flight)
+    const int padded = (total + LS - 1) / LS * LS;   // loader iterations
 
     // the BN affine of every input channel (identity for raw sources), read by the loaders per chunk from LDS
     __shared__ __attribute__((aligned(16))) float sbn[2 * SBN_MAX + 2 * CK];  // + the tail of a partial chunk
@@ -337,7 +339,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         // issued after the halo of chunk g+LS-1 and before that of chunk g+LS.
         // LS register sets: up to LS chunks' halo loads are in flight while the MFMA waves compute another
         // (the 8-channel input, one chunk per item, no weight loads in the loop: LS = 4).
-        constexpr int LS = NT == 1 && CK == 8 ? 4 : 2;
         static_assert(LS == 2 || LS == 4, "set (g % LS) and buffer (g & 1) static per unrolled iteration");
         // one object per set (an array of sets past ~256 B stays in scratch instead of registers)
         struct HSet {
@@ -472,6 +473,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         if (total > 0) {
             // the loads an iteration would have issued before chunk 0: the halo of chunks 0 .. LS-2, the weights
             // of chunk 0, the halo of chunk LS-1 (WCONST: the weights first, stored right away)
+            // sched barriers: the issue order must be an iteration's (the scheduler may swap independent sets)
             geometry();
             if constexpr (WCONST) {
                 load_w();
@@ -479,23 +481,26 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 store_w(1);
             }
             load(S0);
+            __builtin_amdgcn_sched_barrier(0);
             if constexpr (LS == 4) {
                 load(S1);
+                __builtin_amdgcn_sched_barrier(0);
                 load(S2);
+                __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (!WCONST) load_w();
+            __builtin_amdgcn_sched_barrier(0);
             if constexpr (LS == 4) load(S3);
             else load(S1);
-            for (int gi = 0;; gi += LS) {
+            // a multiple of LS iterations, no exit between them (an exit between the sets made the compiler's
+            // vmcnt bookkeeping drain every load in half of them); the iterations past the last chunk store
+            // zeros into buffers the MFMA waves no longer read, and they meet them with extra barriers
+            for (int gi = 0; gi < total; gi += LS) {
                 iter(S0);
-                if (gi + 1 >= total) break;
                 iter(S1);
-                if (gi + 2 >= total) break;
                 if constexpr (LS == 4) {
                     iter(S2);
-                    if (gi + 3 >= total) break;
                     iter(S3);
-                    if (gi + 4 >= total) break;
                 }
             }
         }
@@ -710,6 +715,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             }
         }
     }
+    for (int e = total; e < padded; ++e) __syncthreads();  // the loaders' iterations past the last chunk
     if (DG && p.dbg && lane == 0) {
         unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + wid) * 4;
         d[0] = t_cp;
@@ -1138,33 +1144,31 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
                 *reinterpret_cast<uint4*>(hxs + (xpix0 + (256 / XPP) * i) * XLD + xpiece * 8) =
                     (WG_EXP & 2048) ? q.x[i] : halo_finish_pk(hc, (q.xm >> i) & 1u, q.x[i]);
         };
-        // tile i is in set i & 1 from its load until its store, which happens one tile ahead of the MFMA
-        // waves; each set is refilled right after its store, so two tiles' loads are in flight. Loads are
-        // unconditional (past the range they fetch nothing): with a conditional younger load the compiler
-        // cannot count vmcnt and drains every load before each store
+        // Iteration i stores tile i (set i & 1, loaded two iterations ago) into LDS buffer i & 1 and refills
+        // the set with tile i + 2, then meets the MFMA waves at the barrier before their tile i: two tiles'
+        // loads in flight. Every iteration issues the same loads and waits (past the block's range the
+        // loads are out of range and fetch nothing), and the prologue issues what an iteration would have:
+        // a load or a wait on only some paths makes the compiler's vmcnt bookkeeping drain every load
         constexpr bool DG = (WG_EXP & 1024) != 0;
         unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t1 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
+        auto iter = [&](TSet& q, int buf, int tile) __attribute__((always_inline)) {
+            if (DG) t0 = __builtin_amdgcn_s_memtime();
+            store(q, buf);
+            if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); t_st += t1 - t0; }
+            load(q, tile);
+            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; t0 = t1; }
+            __syncthreads();
+            if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+        };
         load(sa, t_begin);
+        __builtin_amdgcn_sched_barrier(0);  // issue order = an iteration's (the scheduler swapped the sets)
         load(sb, t_begin + 1);
-        if (ntile > 0) store(sa, 0);
-        load(sa, t_begin + 2);
-        __syncthreads();
+        // an even number of iterations (no exit between the two sets: the compiler's vmcnt bookkeeping then
+        // treats both alike); an odd count's last one stores a tile past the range into the buffer the MFMA
+        // waves no longer read, and they meet it with one extra barrier
         for (int i = 0; i < ntile; i += 2) {
-            if (DG) t0 = __builtin_amdgcn_s_memtime();
-            if (i + 1 < ntile) store(sb, 1);
-            if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); t_st += t1 - t0; }
-            load(sb, t_begin + i + 3);
-            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; t0 = t1; }
-            __syncthreads();
-            if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
-            if (i + 1 >= ntile) break;
-            if (DG) t0 = __builtin_amdgcn_s_memtime();
-            if (i + 2 < ntile) store(sa, 0);
-            if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); t_st += t1 - t0; }
-            load(sa, t_begin + i + 4);
-            if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; t0 = t1; }
-            __syncthreads();
-            if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+            iter(sa, 0, t_begin + i + 2);
+            iter(sb, 1, t_begin + i + 3);
         }
         if (DG && p.dbg && lane == 0) {
             unsigned long long* d = p.dbg + ((size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + 4 + wid) * 4;
@@ -1203,9 +1207,14 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
     const char* lds = reinterpret_cast<const char*>(smem);
     constexpr bool DG = (WG_EXP & 1024) != 0;
     unsigned long long t_cp = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
-    __syncthreads();
     for (int it = 0; it < ntile; ++it) {
         if (DG) t0 = __builtin_amdgcn_s_memtime();
+        __syncthreads();  // tile it is in buffer it & 1 (and the loaders may overwrite the other one)
+        if (DG) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_br += t1 - t0;
+            t0 = t1;
+        }
         const unsigned bufb = (unsigned)((it & 1) * BUF * 2);  // byte offset of this buffer
         unsigned abase = bufb + (unsigned)(pc * DLD + co0 + 4 * pp) * 2u;
         asm volatile("" : "+v"(abase));
@@ -1245,14 +1254,9 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if (DG) {
-            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-            t_cp += t1 - t0;
-            t0 = t1;
-        }
-        __syncthreads();
-        if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
+        if (DG) t_cp += __builtin_amdgcn_s_memtime() - t0;
     }
+    if (ntile & 1) __syncthreads();  // the loaders' last (even-count) iteration
     if (DG && p.dbg && lane == 0) {
         unsigned long long* d = p.dbg + ((size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + wid) * 4;
         d[0] = t_cp;
@@ -1313,8 +1317,6 @@ static double halo_chunk_cycles(int th, int tw, int rt, int ck, int nt) {
     const double stores = ((double)(th + 2) * (tw + 2) * ck * 2 + 32.0 * nt * 9 * ck * 2) / 79.0;
     return mfma > reads + stores ? mfma : reads + stores;
 }
-// stats: forward (STATS epilogue) instances carry 32*NT statistics registers, so CK = 16 tiles stop at
-// RT = 3 there; dgrad instances take RT = 4 (512-pixel tiles)
 static HTile halo_tile(int H, int W, int N, bool stats) {
     const int nt = N == 32 ? 1 : 2;
     // CK = 32 (RT <= 3) measured faster than the CK = 16 / 512-pixel tiling at every N % 64 layer of
@@ -1347,7 +1349,7 @@ static HTile halo_tile(int H, int W, int N, bool stats) {
     }
     // CK = 16: search tiles of <= 128*RT pixels (halo within the RT's LDS capacity) minimising the
     // modelled chunk cycles over the image; tw runs over the width, its divisors <= 128 and 32
-    const int rt_max = stats ? 3 : 4;
+    const int rt_max = 4;
     HTile best{8, 32, 2, 16};
     double best_cost = 1e300;
     for (int tw = 1; tw <= (W < 128 ? W : 128); ++tw) {
@@ -1442,8 +1444,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
     p.dbg = g_wg_dbg;
     SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= halo_px_cap(t.rt, t.ck) && t.th * t.tw <= 128 * t.rt &&
-                   t.th < 64 && t.tw < 512 &&
-                   !(st_ && t.rt == 4 && t.ck == 16),
+                   t.th < 64 && t.tw < 512,
                "sd_conv_gemm(halo): tile %dx%d (RT %d, CK %d)", t.th, t.tw, t.rt, t.ck);
     SD_REQUIRE((long long)batch * p.tiles < (1LL << 30), "sd_conv_gemm(halo): too many tiles");
     // 32-bit buffer offsets: image-local halo offsets (24-bit pixel index) and the packed weights
@@ -1465,7 +1466,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
         if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p);
         else launch_halo<2, 2, 32>(st_, wc, grid, st, p);
     } else if (t.rt == 4) {
-        hipLaunchKernelGGL((k_halo_conv<2, 4, 16, false, false>), grid, dim3(512), 0, st, p);
+        launch_halo<2, 4, 16>(st_, wc, grid, st, p);
     } else if (t.rt == 3) {
         launch_halo<2, 3, 16>(st_, wc, grid, st, p);
     } else {
