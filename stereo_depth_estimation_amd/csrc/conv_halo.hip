@@ -409,6 +409,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 unsigned off;
                 asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(hpx[i]), "s"(C * 2), "v"(lpiece * 16));
                 off = ok ? off : OOB;
+                if (WG_EXP & 262144) {
+                    q.hr[i] = make_uint4(off, off, off, off);
+                    continue;
+                }
                 const auto x = __builtin_amdgcn_raw_buffer_load_b128(hrs, off, cl * 2, 0);
                 q.hr[i] = make_uint4(x[0], x[1], x[2], x[3]);
             }
@@ -436,13 +440,13 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 const int item = ltid + i * 256;
                 uint4 v = q.hr[i];
                 const bool ok = (q.m >> i) & 1u;
-                if (q.bn) {
+                if (q.bn && !(WG_EXP & 2048)) {
                     v = bnrelu_pk(v, s0, s1, h0, h1);
                     v = ok ? v : make_uint4(0, 0, 0, 0);  // zero padding after the activation
                 }
                 *reinterpret_cast<uint4*>(hx + ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8) = v;
             }
-            if constexpr (!WCONST) store_w(buf);
+            if constexpr (!WCONST) if (!(WG_EXP & 131072)) store_w(buf);
         };
         constexpr std::integral_constant<int, 0> S0{};
         constexpr std::integral_constant<int, 1> S1{};
@@ -462,10 +466,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         };
         auto iter = [&](auto U) __attribute__((always_inline)) {
             if (DG) t0 = __builtin_amdgcn_s_memtime();
-            store(U, decltype(U)::value & 1);
+            if (!(WG_EXP & 65536)) store(U, decltype(U)::value & 1);
             stamp(t_st);
-            if constexpr (!WCONST) load_w();
-            load(U);
+            if constexpr (!WCONST) if (!(WG_EXP & 65536)) load_w();
+            if (!(WG_EXP & 65536)) load(U);
             stamp(t_ld);
             __syncthreads();
             stamp(t_br);
@@ -590,7 +594,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         const __bf16* wl = hx + HALO_ELEMS;
         // KS k-steps (tap, 16-channel part); fragments are read one step ahead of the MFMAs
         // (register ring) so LDS latency stays behind the matrix core (2 steps measured no faster)
-        constexpr int PF = 1;
+#ifndef HC_PF
+#define HC_PF 1
+#endif
+        constexpr int PF = HC_PF;
         bf16x8 af[PF + 1][RT], bfr[PF + 1][NT];
         auto read_frags = [&](int step) {
             const int slot_ = step % (PF + 1);
