@@ -87,10 +87,12 @@ class GemmTimer:
         n_real = N
         if sb.ptr[0] == xin:
             n_real = sb.taps * eng.in_channels
+        if name == "sd_wgrad_gemm_bnbwd":
+            return 2.0 * B * H * W * M * n_real, L.kernel_name("sd_wgrad_bnbwd_kernel_name", a, sb, M, N)
         return 2.0 * B * H * W * M * n_real, L.kernel_name("sd_wgrad_kernel_name", dt, a, sb, M, N)
 
     def __call__(self, name, args, phase):
-        if name not in ("sd_conv_gemm", "sd_wgrad_gemm"):
+        if name not in ("sd_conv_gemm", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
         ev.record()

@@ -112,6 +112,21 @@ const char* sd_wgrad_kernel_name(int dtype, const sd_src* a, const sd_src* b, in
 int sd_wgrad_splits(int dtype, int batch, int H, int W, int M, int N);
 int sd_wgrad_gemm(int dtype, const sd_src* a, const sd_src* b, int batch, int H, int W, int M, int N, float* slab,
                   int splits, sd_stream s);
+/* The BatchNorm2d backward apply (sd_bn_bwd_apply, model.py:37,40) fused into the bf16 3x3 weight gradient
+ * (convolution_backward wgrad, model.py:36,39): the kernel stages A = dy formed from the raw pair
+ * (da, y) as sd_bn_bwd_apply defines it, dy = coef0*(dz - coef1 - xhat*coef2), dz = da*[scale*y+shift > 0],
+ * xhat = (y-mean)*invstd, and also writes that dy to a->ptr[0] ([pixels][M], for the dgrad). Same b/slab/splits
+ * contract as sd_wgrad_gemm (a: the plain 1x1 [pixels][M] source, used as the dy destination). The kernel
+ * takes coef0 = scale (both are gamma*invstd as sd_bn_fwd_finalize / sd_bn_eval_coeffs and
+ * sd_bn_bwd_finalize write them) and reads coef1, coef2 from coef.
+ * sd_wgrad_bnbwd_ok: 0 when the shape has no fused kernel (then apply + sd_wgrad_gemm), else the number of
+ * x-channel blocks that each form the same dy tile (1: dy is formed once; more: the transform is repeated per
+ * block, which costs more than the separate apply pass at the model's deep layers). */
+int sd_wgrad_bnbwd_ok(int dtype, const sd_src* a, const sd_src* b, int M, int N);
+int sd_wgrad_gemm_bnbwd(int dtype, const sd_src* a, const sd_src* b, int batch, int H, int W, int M, int N,
+                        const void* da, const void* y, const float* scale, const float* shift, const float* mean,
+                        const float* invstd, const float* coef, float* slab, int splits, sd_stream s);
+const char* sd_wgrad_bnbwd_kernel_name(const sd_src* a, const sd_src* b, int M, int N);
 /* sum the slabs and write the PyTorch-layout fp32 gradient:
  *   SD_W_CONV3: M = co, N = 9*ci_pad -> dw[co][ci_real][3][3]
  *   SD_W_CONVT: M = ci, N = 4*co     -> dw[ci][co][2][2] */

@@ -101,6 +101,9 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_wgrad_kernel_name": (ctypes.c_char_p, [_i, _SRC, _SRC, _i, _i]),
     "sd_wgrad_splits": (_i, [_i, _i, _i, _i, _i, _i]),
     "sd_wgrad_gemm": (_i, [_i, _SRC, _SRC, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "sd_wgrad_bnbwd_ok": (_i, [_i, _SRC, _SRC, _i, _i]),
+    "sd_wgrad_gemm_bnbwd": (_i, [_i, _SRC, _SRC, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
+    "sd_wgrad_bnbwd_kernel_name": (ctypes.c_char_p, [_SRC, _SRC, _i, _i]),
     "sd_wgrad_reduce": (_i, [_p, _i, _i, _i, _i, _i, _p, _p]),
     "sd_bn_fwd_finalize": (_i, [_p, _i, _i, _d, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
     "sd_bn_eval_coeffs": (_i, [_p, _p, _p, _p, _i, _f, _p, _p, _p, _p, _p]),
@@ -174,7 +177,7 @@ def kernel_name(name: str, *args) -> str:
 def call(name: str, *args) -> int:
     """Call an int-returning entry point; raise StereoHipError with sd_last_error() on failure."""
     lib = load()
-    if name.endswith(("_rows", "_splits")) or name == "sd_version":
+    if name.endswith(("_rows", "_splits", "_ok")) or name == "sd_version":
         return getattr(lib, name)(*args)
     if _hook is not None:
         _hook(name, args, "pre")

@@ -27,6 +27,13 @@ int sd_check_launch(const char* what);
 
 static inline hipStream_t to_stream(sd_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// BatchNorm-backward operands of the fused weight gradient (sd_wgrad_gemm_bnbwd -> conv_halo.hip)
+struct HaloBnBwd {
+    const void* da;
+    const void* y;
+    const float *scale, *shift, *mean, *invstd, *coef;
+};
+
 // ------------------------------------------------------------------ bilinear source index
 // F.interpolate(mode="bilinear", align_corners=False) as ATen computes it (UpSample.h:
 // area_pixel_compute_source_index + guard_index_and_lambda): s = (in/out)*(o+0.5)-0.5 clamped at

@@ -21,7 +21,8 @@ constexpr int CK = 32;                           // channels per chunk
 #ifndef WG_EXP
 #define WG_EXP 0  // timing experiments only. wgrad<64>: bit 0 no MFMA phase, 1 no tile loads after the first,
                   // 2 no LDS stores; halo conv: bit 3 no MFMA phase, 5 no halo LDS stores, 12 no epilogue stores
-                  // stores; k_halo_wgrad_ws: bit 6 no MFMA phase, 7 no LDS stores, 8 no loads and no stores
+                  // stores; k_halo_wgrad_ws: bit 6 no MFMA phase, 7 no LDS stores, 8 no loads and no stores;
+                  // BNB: bit 19 no dy transform, 20 no dy global stores, 21 no y loads
 #endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -769,6 +770,14 @@ struct HWgArgs {
     float* slab;
     int xcd;           // 1: XCD-contiguous block numbering (block count % 8 == 0)
     unsigned long long* dbg;  // timing-diagnostic builds only (WG_EXP & 1024): per-wave cycle counters
+    // k_halo_wgrad_ws<..., BNB = true>: the BatchNorm-backward apply (sd_bn_bwd_apply) runs in the dy staging.
+    // The loaders read the raw pair (da, y) instead of dy, form dy = k0*(dz - k1 - xhat*k2) (dz = da where
+    // y*scale+shift > 0, xhat = (y-mean)*invstd, coef = {k0, k1, k2} per channel), stage it, and write it to
+    // `dy` for the dgrad: tile t by the x-channel block t % ncc, so every dy piece is written exactly once.
+    const __bf16* bda;
+    const __bf16* by;
+    const float *bsc, *bsh, *bmu, *bis, *bcoef;
+    int ncc;
 };
 
 constexpr int XW_LD = CK + 16;  // halo pixel stride for transposed reads (96 B)
@@ -1015,7 +1024,33 @@ constexpr int WS_PD = 5;                        // tap-steps of fragment read-ah
 // tiles carry little MFMA work and need more loads in flight; one otherwise
 __host__ __device__ constexpr int ws_blocks_per_cu(int cout, int cib) { return cout == 32 && cib == 32 ? 2 : 1; }
 
-template <int COUT, int CIB, int HP, int HR>  // dy / x channels per block; halo pitch and rows (tw+2 <= HP, th+2 <= HR)
+// dy for 8 channels from the raw bf16 pieces (da, y): the BatchNorm-backward apply of k_bn_bwd_apply,
+// dy = k0*(dz - k1 - xhat*k2), dz = da where z = y*scale+shift > 0 (the forward ReLU mask, recomputed as
+// k_bn_bwd_apply does), xhat = (y-mean)*invstd, written in terms of z (which the mask needs anyway) with
+// k0 = scale: dy = scale*dz + Bz*z + Cz, Bz = -invstd*k2, Cz = invstd*k2*shift + scale*(mean*invstd*k2 - k1)
+__device__ __forceinline__ uint4 bn_bwd_pk(uint4 da, uint4 y, const float* sc, const float* sh, const float* Bz,
+                                           const float* Cz) {
+    const unsigned dw[4] = {da.x, da.y, da.z, da.w}, yw[4] = {y.x, y.y, y.z, y.w};
+    unsigned o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = 2 * i + h;
+            const float yv = __uint_as_float(h ? yw[i] & 0xffff0000u : yw[i] << 16);
+            const float dv = __uint_as_float(h ? dw[i] & 0xffff0000u : dw[i] << 16);
+            const float z = __builtin_fmaf(yv, sc[c], sh[c]);
+            const float t = __builtin_fmaf(Bz[c], z, Cz[c]);
+            r[h] = z > 0.f ? __builtin_fmaf(sc[c], dv, t) : t;
+        }
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(o[i]) : "v"(r[0]), "v"(r[1]));
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int COUT, int CIB, int HP, int HR, bool BNB>  // dy / x channels per block; halo pitch and rows (tw+2 <= HP,
+                                                       // th+2 <= HR); BNB: BatchNorm-backward apply in the dy staging
 __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_wgrad_ws(const HWgArgs p) {
     constexpr int KS = WS_TPX / 32;
     constexpr int NCI = CIB / 16, NCO = 4 / NCI, RM = COUT / 16 / NCO;  // wave grid and 16-row tiles per wave
@@ -1096,9 +1131,30 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             const unsigned gg = (hgeo[i / 2] >> (16 * (i & 1))) & 0xffffu;
             xpo[i] = (((int)(gg >> 8) - 1) * p.W + (int)(gg & 0xff) - 1) * xC + hc.c;
         }
+        // BNB: this thread's 8 dy channels (fixed piece) -> the folded BatchNorm-backward constants
+        constexpr int NK = BNB ? 8 : 1;
+        float ksc[NK], ksh[NK], kB[NK], kC[NK];
+        if constexpr (BNB) {
+            const int c = mb + dpiece * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float k1 = p.bcoef[3 * (c + j) + 1], k2 = p.bcoef[3 * (c + j) + 2];
+                const float is = p.bis[c + j], sc = p.bsc[c + j], sh = p.bsh[c + j];
+                ksc[j] = sc;
+                ksh[j] = sh;
+                kB[j] = -is * k2;
+                kC[j] = is * k2 * sh + sc * (p.bmu[c + j] * is * k2 - k1);
+            }
+        }
+        constexpr int DYY = BNB ? DYP : 1;
+        constexpr unsigned OOB = 0x80000000u;
         struct TSet {
             uint4 d[DYP], x[HXP];
-            unsigned xm;
+            unsigned xm;   // bit i: halo piece i inside the image; BNB: bit 16 + i: dy piece i inside the tile
+            uint4 y[DYY];  // BNB: the raw y pieces beside da in d
+            int dbase;     // BNB: element offset of the tile origin in its image
+            int img;       // BNB: the tile's image
+            bool wr;       // BNB: this block writes the tile's dy
         };
         TSet sa, sb;
         auto load = [&](TSet& q, int tile) __attribute__((always_inline)) {
@@ -1110,8 +1166,14 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             const size_t img = (size_t)b * p.H * p.W;
             const int tpx = h0 * p.W + w0;
             const int nimg = p.H * p.W;
-            const __amdgpu_buffer_rsrc_t rdy =
-                __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + img * p.M), (short)0, nimg * p.M * 2, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)((BNB ? p.bda : p.dy) + img * p.M), (short)0, nimg * p.M * 2, 0x00020000);
+            const __amdgpu_buffer_rsrc_t ryr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)((BNB ? p.by : p.dy) + img * p.M), (short)0, BNB ? nimg * p.M * 2 : 0, 0x00020000);
+            if constexpr (BNB) {
+                q.img = b;
+                q.wr = tile % p.ncc == cc;
+            }
             const __amdgpu_buffer_rsrc_t rx =
                 __builtin_amdgcn_make_buffer_rsrc((void*)(xsrc + img * xC), (short)0, nimg * xC * 2, 0x00020000);
             // halo piece (hy, hx) is inside the image iff 1 - h0 <= hy < H - h0 + 1 and 1 - w0 <= hx < W - w0 + 1
@@ -1123,10 +1185,21 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             for (int i = 0; i < DYP; ++i) {
                 const unsigned rc = (dyrc[i / 2] >> (16 * (i & 1))) & 0xffffu;
                 const bool ok = (rc != 0xffffu) & ((int)(rc >> 8) < rhi - 1) & ((int)(rc & 0xff) < chi - 1) & (rhi > rlo);
-                const unsigned off = ok ? (unsigned)(dbase + dpo[i]) * 2u : 0x80000000u;
+                const unsigned off = ok ? (unsigned)(dbase + dpo[i]) * 2u : OOB;
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(rdy, off, 0, 0);
                 q.d[i] = make_uint4(v[0], v[1], v[2], v[3]);
+                if constexpr (BNB) {
+                    if (WG_EXP & 2097152) {  // timing experiment: no y loads
+                        q.y[i] = q.d[i];
+                        xm |= (unsigned)ok << (16 + i);
+                        continue;
+                    }
+                    const auto u = __builtin_amdgcn_raw_buffer_load_b128(ryr, off, 0, 0);
+                    q.y[i] = make_uint4(u[0], u[1], u[2], u[3]);
+                    xm |= (unsigned)ok << (16 + i);
+                }
             }
+            if constexpr (BNB) q.dbase = dbase;
 #pragma unroll
             for (int i = 0; i < HXP; ++i) {
                 const unsigned gg = (hgeo[i / 2] >> (16 * (i & 1))) & 0xffffu;
@@ -1143,9 +1216,26 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             if (WG_EXP & (128 | 256)) return;
             __bf16* dys = smem + buf * BUF;
             __bf16* hxs = dys + DY_E;
+            if constexpr (BNB) {
+                // dy pieces outside the tile are zero (the raw pair loaded as zeros gives dy = C there); the
+                // writer block also stores them (buffer stores: out-of-range pieces dropped, no branch)
+                const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(p.dy + (size_t)q.img * p.H * p.W * p.M), (short)0, p.H * p.W * p.M * 2, 0x00020000);
 #pragma unroll
-            for (int i = 0; i < DYP; ++i)  // out-of-range pieces were loaded as zeros
-                *reinterpret_cast<uint4*>(dys + (dpix0 + (256 / DPP) * i) * DLD + dpiece * 8) = q.d[i];
+                for (int i = 0; i < DYP; ++i) {
+                    const bool ok = (q.xm >> (16 + i)) & 1u;
+                    uint4 v = (WG_EXP & 524288) ? q.d[i] : bn_bwd_pk(q.d[i], q.y[i], ksc, ksh, kB, kC);
+                    v = ok ? v : make_uint4(0, 0, 0, 0);
+                    *reinterpret_cast<uint4*>(dys + (dpix0 + (256 / DPP) * i) * DLD + dpiece * 8) = v;
+                    __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
+                    const unsigned off = (ok & q.wr) ? (unsigned)(q.dbase + dpo[i]) * 2u : OOB;
+                    if (!(WG_EXP & 1048576)) __builtin_amdgcn_raw_buffer_store_b128(data, rdo, off, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < DYP; ++i)  // out-of-range pieces were loaded as zeros
+                    *reinterpret_cast<uint4*>(dys + (dpix0 + (256 / DPP) * i) * DLD + dpiece * 8) = q.d[i];
+            }
 #pragma unroll
             for (int i = 0; i < HXP; ++i)
                 *reinterpret_cast<uint4*>(hxs + (xpix0 + (256 / XPP) * i) * XLD + xpiece * 8) =
@@ -1573,25 +1663,40 @@ int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
     return splits < 1 ? 1 : splits;
 }
 
-const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W) {
+const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W, bool bnb) {
     static thread_local char buf[64];
     const WsCfg ws = wgrad_ws(M, N, c0);
     if (!ws.cib) return M == 32 ? "k_halo_wgrad<32>" : "k_halo_wgrad<64>";
     const WsTile t = wgrad_tile_ws(H, W);
-    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d>", ws.cout, ws.cib, t.hp, t.hr);
+    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false");
     return buf;
 }
 
-template <int COUT, int CIB>
+template <int COUT, int CIB, bool BNB>
 static void launch_wgrad_ws(int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
     if (hp == 34)
-        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6, BNB>), grid, dim3(512), 0, st, p);
     else
-        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8, BNB>), grid, dim3(512), 0, st, p);
+}
+template <bool BNB>
+static void launch_wgrad_ws(const WsCfg& ws, int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
+    if (ws.cout == 64 && ws.cib == 64) launch_wgrad_ws<64, 64, BNB>(hp, grid, st, p);
+    else if (ws.cout == 64) launch_wgrad_ws<64, 32, BNB>(hp, grid, st, p);
+    else if (ws.cib == 64) launch_wgrad_ws<32, 64, BNB>(hp, grid, st, p);
+    else launch_wgrad_ws<32, 32, BNB>(hp, grid, st, p);
+}
+
+// the BatchNorm-backward apply fused into the dy staging: warp-specialised instances only. Returns the number
+// of x-channel blocks (grid.x) that each form the same dy tile (0: no fused kernel for the shape)
+int sd_halo_wgrad_bnbwd_blocks(const sd_src& a, const sd_src& b, int M, int N) {
+    if (!sd_halo_wgrad_ok(a, b, M)) return 0;
+    const WsCfg ws = wgrad_ws(M, N, b.chans[0]);
+    return ws.cib ? (N / 9) / ws.cib : 0;
 }
 
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
-                  hipStream_t st) {
+                  hipStream_t st, const HaloBnBwd* bnb) {
     const WsCfg ws = wgrad_ws(M, N, b.chans[0]);  // one source per block of x channels
     const WsTile wt = wgrad_tile_ws(H, W);
     const HTile t = ws.cib ? HTile{wt.th, wt.tw, 4, 32} : wgrad_tile(H, W);
@@ -1612,17 +1717,32 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
     p.N = N;
     p.slab = slab;
     p.dbg = g_wg_dbg;
+    p.bda = p.by = nullptr;
+    p.bsc = p.bsh = p.bmu = p.bis = p.bcoef = nullptr;
+    p.ncc = 1;
+    if (bnb && !ws.cib) {
+        sd_set_error("sd_wgrad_gemm_bnbwd: no fused kernel for M=%d N=%d", M, N);
+        return SD_EINVAL;
+    }
+    if (bnb) {
+        p.bda = (const __bf16*)bnb->da;
+        p.by = (const __bf16*)bnb->y;
+        p.bsc = bnb->scale;
+        p.bsh = bnb->shift;
+        p.bmu = bnb->mean;
+        p.bis = bnb->invstd;
+        p.bcoef = bnb->coef;
+    }
     if (ws.cib) {
         const int ncc = p.x.ctot / ws.cib;
         p.xcd = halo_xcd_enabled() && (ncc * splits * (M / ws.cout)) % 8 == 0;
         SD_REQUIRE(t.th + 2 <= wt.hr && t.tw + 2 <= wt.hp && t.th * t.tw <= WS_TPX, "sd_wgrad_gemm(halo ws): tile %dx%d",
                    t.th, t.tw);
         const dim3 grid(ncc, splits, M / ws.cout);
-        if (ws.cout == 64 && ws.cib == 64) launch_wgrad_ws<64, 64>(wt.hp, grid, st, p);
-        else if (ws.cout == 64) launch_wgrad_ws<64, 32>(wt.hp, grid, st, p);
-        else if (ws.cib == 64) launch_wgrad_ws<32, 64>(wt.hp, grid, st, p);
-        else launch_wgrad_ws<32, 32>(wt.hp, grid, st, p);
-        return sd_check_launch("sd_wgrad_gemm(halo ws)");
+        p.ncc = ncc;
+        if (bnb) launch_wgrad_ws<true>(ws, wt.hp, grid, st, p);
+        else launch_wgrad_ws<false>(ws, wt.hp, grid, st, p);
+        return sd_check_launch(bnb ? "sd_wgrad_gemm_bnbwd(halo ws)" : "sd_wgrad_gemm(halo ws)");
     }
     p.xcd = halo_xcd_enabled() && (cdiv(p.x.ctot, CK) * splits * (M == 32 ? 1 : M / 64)) % 8 == 0;
     SD_REQUIRE(p.nhalo <= HMAX && t.th * t.tw <= WG_MAXPX, "sd_wgrad_gemm(halo): tile %dx%d", t.th, t.tw);

@@ -259,13 +259,15 @@ int sd_fast_wgrad_gemm(const sd_src& a, const sd_src& b, int batch, int H, int W
 bool sd_halo_wgrad_ok(const sd_src& a, const sd_src& b, int M);
 bool sd_halo_wgrad_shape(int M, int N);
 int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N);
-const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W);
+const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W, bool bnb);
+int sd_halo_wgrad_bnbwd_blocks(const sd_src& a, const sd_src& b, int M, int N);
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
-                  hipStream_t st);
+                  hipStream_t st, const HaloBnBwd* bnb = nullptr);
 
 extern "C" const char* sd_wgrad_kernel_name(int dtype, const sd_src* a, const sd_src* b, int M, int N) {
     static thread_local char buf[96];
-    if (dtype == SD_BF16 && a && b && sd_halo_wgrad_ok(*a, *b, M)) return sd_halo_wgrad_name(M, N, b->chans[0], a->H, a->W);
+    if (dtype == SD_BF16 && a && b && sd_halo_wgrad_ok(*a, *b, M))
+        return sd_halo_wgrad_name(M, N, b->chans[0], a->H, a->W, false);
     if (dtype == SD_BF16 && a && b && !a->pool && !b->pool) return sd_fast_wgrad_name(M, N);
     const WCfg c = pick_wcfg(M, N);
     snprintf(buf, sizeof(buf), "k_wgemm<%s, %d, %d, 2, 2>", dtype == SD_BF16 ? "__bf16" : "float", c.bm, c.bn);
@@ -318,6 +320,35 @@ extern "C" int sd_wgrad_gemm(int dtype, const sd_src* a, const sd_src* b, int ba
     }
     WgArgs<float> p{ga, gb, H, W, (int)P, M, N, pps, slab};
     return launch_wg(p, splits, to_stream(s));
+}
+
+extern "C" int sd_wgrad_bnbwd_ok(int dtype, const sd_src* a, const sd_src* b, int M, int N) {
+    return dtype == SD_BF16 && a && b ? sd_halo_wgrad_bnbwd_blocks(*a, *b, M, N) : 0;
+}
+
+extern "C" const char* sd_wgrad_bnbwd_kernel_name(const sd_src* a, const sd_src* b, int M, int N) {
+    if (!a || !b || !sd_halo_wgrad_bnbwd_blocks(*a, *b, M, N)) return "";
+    return sd_halo_wgrad_name(M, N, b->chans[0], a->H, a->W, true);
+}
+
+extern "C" int sd_wgrad_gemm_bnbwd(int dtype, const sd_src* a, const sd_src* b, int batch, int H, int W, int M, int N,
+                                   const void* da, const void* y, const float* scale, const float* shift,
+                                   const float* mean, const float* invstd, const float* coef, float* slab, int splits,
+                                   sd_stream s) {
+    if (int e = sd_validate_src(a, "sd_wgrad_gemm_bnbwd(a)")) return e;
+    if (int e = sd_validate_src(b, "sd_wgrad_gemm_bnbwd(b)")) return e;
+    SD_REQUIRE(dtype == SD_BF16, "sd_wgrad_gemm_bnbwd: bf16 only (dtype %d)", dtype);
+    SD_REQUIRE(slab && splits > 0 && batch > 0 && H > 0 && W > 0, "sd_wgrad_gemm_bnbwd: bad args");
+    SD_REQUIRE(da && y && scale && shift && mean && invstd && coef && a->ptr[0], "sd_wgrad_gemm_bnbwd: null pointer");
+    SD_REQUIRE(a->taps == 1 && a->chans[0] == M && a->chans[1] == 0 && a->H == H && a->W == W && !a->scale[0],
+               "sd_wgrad_gemm_bnbwd: A must be the plain 1x1 dy destination [pixels][M] on the grid");
+    SD_REQUIRE(b->taps == 9 && b->H == H && b->W == W && (b->chans[0] + b->chans[1]) * 9 == N,
+               "sd_wgrad_gemm_bnbwd: B must be the 3x3 x source on the grid (N = 9 * channels)");
+    SD_REQUIRE((long long)batch * H * W < (1LL << 31), "sd_wgrad_gemm_bnbwd: too many pixels");
+    SD_REQUIRE(sd_halo_wgrad_bnbwd_blocks(*a, *b, M, N) > 0, "sd_wgrad_gemm_bnbwd: no fused kernel for M=%d N=%d", M,
+               N);
+    const HaloBnBwd bn{da, y, scale, shift, mean, invstd, coef};
+    return sd_halo_wgrad(*a, *b, batch, H, W, M, N, slab, splits, to_stream(s), &bn);
 }
 
 extern "C" int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw,

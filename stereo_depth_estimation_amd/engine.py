@@ -13,6 +13,7 @@ the host, so a whole step can be captured into a HIP graph (torch.cuda.CUDAGraph
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -151,6 +152,8 @@ class UNetEngine:
         self.adam_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_scratch = torch.zeros(4, dtype=torch.float32, device=dev)
         self.ws: Workspace | None = None
+        # bf16 training: BatchNorm-backward apply fused into the weight gradients (SD_BN_FUSE=0: separate pass)
+        self.bn_fuse = os.environ.get("SD_BN_FUSE", "1") != "0"
         self.params: dict[str, torch.Tensor] = {}
         self.grads: dict[str, torch.Tensor] = {}
         self.bufs: dict[str, torch.Tensor] = {}
@@ -511,9 +514,10 @@ class UNetEngine:
         """sd_pool_bwd_add can produce this layer's BN-backward sums (C/8 must divide 256)."""
         return 256 % (cl.cout // 8) == 0
 
-    def _bn_bwd(self, cl: ConvL, fused_rows: int = 0):
+    def _bn_bwd(self, cl: ConvL, fused_rows: int = 0, apply: bool = True):
         """da:<cl> -> dy:<cl>, dgamma/dbeta (model.py:37,40 BatchNorm2d backward, ReLU mask fused).
-        fused_rows > 0: the producer of da already wrote that many partial-sum rows into t["chan"]."""
+        fused_rows > 0: the producer of da already wrote that many partial-sum rows into t["chan"].
+        apply=False: only the sums and coefficients; the weight gradient forms dy while staging it."""
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         P = ws.B * (ws.H >> cl.level) * (ws.W >> cl.level)
         args = (t["scale:" + cl.name].data_ptr(), t["shift:" + cl.name].data_ptr(), t["mean:" + cl.name].data_ptr(),
@@ -530,8 +534,9 @@ class UNetEngine:
                self.params[cl.bn_key + ".weight"].data_ptr(), t["invstd:" + cl.name].data_ptr(),
                int(ws.fwd_train), self.grads[cl.bn_key + ".weight"].data_ptr(), self.grads[cl.bn_key + ".bias"].data_ptr(),
                coef.data_ptr(), s)
-        L.call("sd_bn_bwd_apply", dt, t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), *args,
-               coef.data_ptr(), P, cl.cout, t["dy:" + cl.name].data_ptr(), s)
+        if apply:
+            L.call("sd_bn_bwd_apply", dt, t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), *args,
+                   coef.data_ptr(), P, cl.cout, t["dy:" + cl.name].data_ptr(), s)
 
     def _wgrad(self, a: L.SdSrc, b: L.SdSrc, lvl: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor):
         ws, s, dt = self.ws, self._s(), self.sd_dtype
@@ -544,8 +549,26 @@ class UNetEngine:
     def _conv_bwd(self, cl: ConvL, need_dgrad: bool, fused_rows: int = 0):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         Hl, Wl = ws.H >> cl.level, ws.W >> cl.level
-        self._bn_bwd(cl, fused_rows)
         dy = t["dy:" + cl.name]
+        a = L.make_src(dy, cl.cout, Hl, Wl, taps=1)
+        b = self._src_fwd(cl)
+        M, N = cl.cout, 9 * cl.cin_pad
+        # bf16: the weight gradient applies the BatchNorm backward while staging dy (and writes dy for the
+        # dgrad), so the apply pass over (da, y) -> dy is gone; it runs first, the dgrad reads its dy. Each
+        # x-channel block of the kernel repeats the transform of the same dy tile on its loader waves, whose VALU
+        # then paces the kernel: fused where one block covers x (two at full resolution, where the separate pass
+        # costs most). Measured per layer (tools/bench_variants.sh): enc1-enc3.0, dec2.1, dec1 gain; deeper lose.
+        nblk = L.call("sd_wgrad_bnbwd_ok", dt, a, b, M, N) if self.bn_fuse and dt == L.SD_BF16 else 0
+        fuse = nblk == 1 or (nblk == 2 and cl.level == 0)
+        self._bn_bwd(cl, fused_rows, apply=not fuse)
+        if fuse:
+            sp = L.call("sd_wgrad_splits", dt, ws.B, Hl, Wl, M, N)
+            slab = t["slab"]
+            L.call("sd_wgrad_gemm_bnbwd", dt, a, b, ws.B, Hl, Wl, M, N, t["da:" + cl.name].data_ptr(),
+                   t["y:" + cl.name].data_ptr(), t["scale:" + cl.name].data_ptr(), t["shift:" + cl.name].data_ptr(),
+                   t["mean:" + cl.name].data_ptr(), t["invstd:" + cl.name].data_ptr(),
+                   t["coef:" + cl.name].data_ptr(), slab.data_ptr(), sp, s)
+            L.call("sd_wgrad_reduce", slab.data_ptr(), sp, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key].data_ptr(), s)
         if need_dgrad:
             dsrc = L.make_src(dy, cl.cout, Hl, Wl, taps=9)
             if cl.idx == 1:
@@ -560,9 +583,8 @@ class UNetEngine:
                 up = self.ups[UP_OF_DEC[cl.blk]]
                 L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d, L.SD_EPI_SPLIT,
                        t["du:" + up.name].data_ptr(), t["dskip:" + up.name].data_ptr(), up.cout, None, None, s)
-        a = L.make_src(dy, cl.cout, Hl, Wl, taps=1)
-        b = self._src_fwd(cl)
-        self._wgrad(a, b, cl.level, cl.cout, 9 * cl.cin_pad, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key])
+        if not fuse:
+            self._wgrad(a, b, cl.level, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key])
 
     def _up_bwd(self, u: UpL):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype

@@ -207,6 +207,51 @@ def test_conv3x3_wgrad_bn_relu_source(B, H, W, ci, co):
     assert float((dw.cpu() - ref).abs().max()) <= 1e-2 * (1 + float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 30, 40, 128, 64), (1, 15, 20, 128, 128), (2, 10, 14, 32, 64),
+                                         (1, 24, 64, 32, 32), (1, 16, 64, 64, 32), (3, 17, 33, 64, 64),
+                                         (1, 48, 64, 32, 32), (2, 15, 20, 256, 64)])
+def test_conv3x3_wgrad_fused_bn_backward(B, H, W, ci, co):
+    """sd_wgrad_gemm_bnbwd: dy = BatchNorm-backward apply of (da, y) formed while staging (written out for the
+    dgrad) and the weight gradient on it, vs sd_bn_bwd_apply's formula in fp32 then F.conv2d backward."""
+    lib = L()
+    torch.manual_seed(5)
+    yx = torch.randn(B, ci, H, W).to(torch.bfloat16).float()
+    scx = (torch.rand(ci) + 0.5) * torch.where(torch.rand(ci) < 0.2, -1.0, 1.0)
+    shx = torch.randn(ci) * 0.3
+    x = torch.relu(yx * scx.view(1, -1, 1, 1) + shx.view(1, -1, 1, 1)).to(torch.bfloat16).float()
+    # BatchNorm backward operands of the conv's output layer: raw output y, upstream gradient da
+    y = (torch.randn(B, co, H, W) * 2 + 0.5).to(torch.bfloat16).float()
+    da = torch.randn(B, co, H, W).to(torch.bfloat16).float()
+    mean, invstd = torch.randn(co) * 0.5, torch.rand(co) + 0.5
+    gamma = (torch.rand(co) + 0.5) * torch.where(torch.rand(co) < 0.2, -1.0, 1.0)
+    sc = gamma * invstd
+    sh = torch.randn(co) * 0.2 - mean * sc
+    coef = torch.stack([sc, torch.randn(co) * 0.1, torch.randn(co) * 0.1], 1).contiguous()
+    v = lambda t: t.view(1, -1, 1, 1)  # noqa: E731
+    dz = torch.where(y * v(sc) + v(sh) > 0, da, torch.zeros_like(da))
+    dy_ref = v(coef[:, 0]) * (dz - v(coef[:, 1]) - (y - v(mean)) * v(invstd) * v(coef[:, 2]))
+    w = torch.zeros(co, ci, 3, 3, requires_grad=True)
+    F.conv2d(x, w, padding=1).backward(dy_ref)
+    dyd = torch.full((B * H * W, co), float("nan"), dtype=torch.bfloat16, device=DEV)
+    dev = [t.to(DEV).contiguous() for t in (sc, sh, mean, invstd, coef)]
+    a = lib.make_src(dyd, co, H, W, taps=1)
+    b = lib.make_src(_nhwc(yx, "bf16"), ci, H, W, taps=9, bn0=(scx.to(DEV), shx.to(DEV)))
+    assert lib.call("sd_wgrad_bnbwd_ok", lib.SD_BF16, a, b, co, 9 * ci) == (ci // 64 if ci % 64 == 0 else ci // 32)
+    sp = lib.call("sd_wgrad_splits", lib.SD_BF16, B, H, W, co, 9 * ci)
+    slab = torch.empty(sp * co * 9 * ci, device=DEV)
+    dw = torch.empty(co, ci, 3, 3, device=DEV)
+    dad, yd = _nhwc(da, "bf16"), _nhwc(y, "bf16")
+    lib.call("sd_wgrad_gemm_bnbwd", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, dad.data_ptr(), yd.data_ptr(),
+             *[t.data_ptr() for t in dev], slab.data_ptr(), sp, lib.stream_handle())
+    lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(), lib.stream_handle())
+    got_dy = _from_nhwc(dyd, B, H, W, co)
+    # every dy element written once (no NaN left), each within bf16 rounding of the fp32 formula
+    assert not torch.isnan(got_dy).any()
+    assert float(((got_dy - dy_ref).abs() - 2 ** -8 * dy_ref.abs()).max()) <= 1e-5 * (1 + float(dy_ref.abs().max()))
+    ref = w.grad
+    assert float((dw.cpu() - ref).abs().max()) <= 1e-2 * (1 + float(ref.abs().max()))
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,h,w_,ci,co", [(2, 5, 7, 32, 16), (2, 12, 20, 64, 32), (1, 15, 20, 128, 64),
                                           # k_convt_fwd: many 128-pixel tiles per block, ragged last tile,

@@ -77,11 +77,33 @@ def test_planning_queries_are_host_only():
     sp = L.call("sd_wgrad_splits", L.SD_BF16, 64, 240, 320, 32, 288)
     assert 1 <= sp <= 64 * 240 * 320 // 256
     assert L.call("sd_chan_reduce_rows", 1000, 32) >= 1
+    # BatchNorm-backward apply fused into the warp-specialised weight gradients (every 3x3 wgrad but enc1.0's)
+    dy = L.make_src(ctypes.c_void_p(16), 32, 240, 320, taps=1)
+    assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy, src, 32, 288) == 1
+    assert L.kernel_name("sd_wgrad_bnbwd_kernel_name", dy, src, 32, 288) == "k_halo_wgrad_ws<32, 32, 22, 8, true>"
+    x256 = L.make_src(ctypes.c_void_p(16), 256, 60, 80, taps=9)
+    dy128 = L.make_src(ctypes.c_void_p(16), 128, 60, 80, taps=1)
+    assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy128, x256, 128, 2304) == 4  # four 64-channel x blocks
+    x8 = L.make_src(ctypes.c_void_p(16), 8, 240, 320, taps=9)
+    assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy, x8, 32, 72) == 0
+    assert L.call("sd_wgrad_bnbwd_ok", L.SD_F32, dy, src, 32, 288) == 0
     # fp8 inference convs (live app, 960x720): one min/max row per persistent block
     assert L.call("sd_conv3x3_fp8_rows", 1, 720, 960, 32) == 256
     assert L.call("sd_conv3x3_fp8_rows", 1, 45, 60, 512) == 12  # 4x60 tiles, 8 N-blocks
     assert L.kernel_name("sd_conv3x3_fp8_kernel_name", 64) == "k_halo_conv_fp8<2>"
     assert L.call("sd_chan_minmax_rows", 691200, 32) == 256
+
+
+def test_fused_bn_wgrad_host_validation():
+    dy = L.make_src(ctypes.c_void_p(16), 32, 24, 32, taps=1)
+    x8 = L.make_src(ctypes.c_void_p(16), 8, 24, 32, taps=9)
+    with pytest.raises(L.StereoHipError, match="no fused kernel"):
+        L.call("sd_wgrad_gemm_bnbwd", L.SD_BF16, dy, x8, 1, 24, 32, 32, 72, 1, 1, 1, 1, 1, 1, 1, 1, 1, None)
+    x = L.make_src(ctypes.c_void_p(16), 32, 24, 32, taps=9)
+    with pytest.raises(L.StereoHipError, match="bf16 only"):
+        L.call("sd_wgrad_gemm_bnbwd", L.SD_F32, dy, x, 1, 24, 32, 32, 288, 1, 1, 1, 1, 1, 1, 1, 1, 1, None)
+    with pytest.raises(L.StereoHipError, match="null pointer"):
+        L.call("sd_wgrad_gemm_bnbwd", L.SD_BF16, dy, x, 1, 24, 32, 32, 288, None, 1, 1, 1, 1, 1, 1, 1, 1, None)
 
 
 def test_fp8_host_validation():
