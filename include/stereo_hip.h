@@ -118,7 +118,8 @@ int sd_wgrad_gemm(int dtype, const sd_src* a, const sd_src* b, int batch, int H,
  * xhat = (y-mean)*invstd, and also writes that dy to a->ptr[0] ([pixels][M], for the dgrad). Same b/slab/splits
  * contract as sd_wgrad_gemm (a: the plain 1x1 [pixels][M] source, used as the dy destination). The kernel
  * takes coef0 = scale (both are gamma*invstd as sd_bn_fwd_finalize / sd_bn_eval_coeffs and
- * sd_bn_bwd_finalize write them) and reads coef1, coef2 from coef.
+ * sd_bn_bwd_finalize write them) and reads coef1, coef2 from coef. a->ptr[0] may be NULL: dy is not written
+ * (a layer without a dgrad); the shapes with x channels not a multiple of 32 (M = 32 only) require that.
  * sd_wgrad_bnbwd_ok: 0 when the shape has no fused kernel (then apply + sd_wgrad_gemm), else the number of
  * x-channel blocks that each form the same dy tile (1: dy is formed once; more: the transform is repeated per
  * block, which costs more than the separate apply pass at the model's deep layers). */

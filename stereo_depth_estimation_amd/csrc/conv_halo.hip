@@ -802,8 +802,33 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* a0, const __bf16* a1) {
     return r;
 }
 
-template <int COUT>
-__global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
+// dy for 8 channels from the raw bf16 pieces (da, y): the BatchNorm-backward apply of k_bn_bwd_apply,
+// dy = k0*(dz - k1 - xhat*k2), dz = da where z = y*scale+shift > 0 (the forward ReLU mask, recomputed as
+// k_bn_bwd_apply does), xhat = (y-mean)*invstd, written in terms of z (which the mask needs anyway) with
+// k0 = scale: dy = scale*dz + Bz*z + Cz, Bz = -invstd*k2, Cz = invstd*k2*shift + scale*(mean*invstd*k2 - k1)
+__device__ __forceinline__ uint4 bn_bwd_pk(uint4 da, uint4 y, const float* sc, const float* sh, const float* Bz,
+                                           const float* Cz) {
+    const unsigned dw[4] = {da.x, da.y, da.z, da.w}, yw[4] = {y.x, y.y, y.z, y.w};
+    unsigned o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = 2 * i + h;
+            const float yv = __uint_as_float(h ? yw[i] & 0xffff0000u : yw[i] << 16);
+            const float dv = __uint_as_float(h ? dw[i] & 0xffff0000u : dw[i] << 16);
+            const float z = __builtin_fmaf(yv, sc[c], sh[c]);
+            const float t = __builtin_fmaf(Bz[c], z, Cz[c]);
+            r[h] = z > 0.f ? __builtin_fmaf(sc[c], dv, t) : t;
+        }
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(o[i]) : "v"(r[0]), "v"(r[1]));
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int COUT, bool BNB>  // BNB: BatchNorm-backward apply in the dy staging (no dy written: enc1.0 has no dgrad)
+__global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // two blocks per CU (LDS: 63-80 KB)
     constexpr int DY_LD = COUT + 16;             // 96 B / 160 B rows: conflict-free transposed reads
     constexpr int RM = COUT / 32;                // 16-row tiles of output channels per wave
     constexpr int DY_PIECES = WG_MAXPX * (COUT / 8);
@@ -812,6 +837,9 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
     __shared__ __attribute__((aligned(16))) __bf16 smem[DY_ELEMS + HX_ELEMS];
     __shared__ int hoff[WG_MAXPX + 8];           // halo offset of flattened pixel m (tap (0,0))
     __shared__ int prc[WG_MAXPX];                // (row << 16 | col) of pixel m, -1 past the tile
+    // BNB: the folded BatchNorm-backward constants of the block's dy channels (scale, shift, Bz, Cz; bn_bwd_pk),
+    // read per tile (in registers they would cost the kernel its second wave per SIMD)
+    __shared__ __attribute__((aligned(16))) float kbn[BNB ? 4 * COUT : 4];
     __bf16* dys = smem;
     __bf16* hxs = smem + DY_ELEMS;
 
@@ -844,6 +872,17 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
         hoff[m] = in ? hm * p.hw + wm : 0;
         if (m < WG_MAXPX) prc[m] = in ? (hm << 16 | wm) : -1;
     }
+    if constexpr (BNB) {
+        for (int j = tid; j < COUT; j += 256) {
+            const int c = mb + j;
+            const float k1 = p.bcoef[3 * c + 1], k2 = p.bcoef[3 * c + 2];
+            const float is = p.bis[c], sc = p.bsc[c], sh = p.bsh[c];
+            kbn[j] = sc;
+            kbn[COUT + j] = sh;
+            kbn[2 * COUT + j] = -is * k2;
+            kbn[3 * COUT + j] = is * k2 * sh + sc * (p.bmu[c] * is * k2 - k1);
+        }
+    }
     int hgeo[HP_PER_THREAD];                     // (row << 16 | col) of this thread's halo pieces
 #pragma unroll
     for (int i = 0; i < HP_PER_THREAD; ++i) {
@@ -862,10 +901,12 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
     // Register sets for the tiles in flight (global -> registers) while a tile is in the matrix core:
     // two for M = 32 (one tile of cover was shorter than an HBM round trip at full resolution; three
     // measured no faster)
-    constexpr int WS = COUT == 32 ? 2 : 1;
+    // (BNB: one, the raw (da, y) pair of a second set does not fit beside the halo in two waves per SIMD)
+    constexpr int WS = COUT == 32 && !BNB ? 2 : 1;
     uint4 dr[WS][DY_PER_THREAD], xr[WS][HP_PER_THREAD];
+    uint4 yr[BNB ? WS : 1][BNB ? DY_PER_THREAD : 1];  // BNB: the raw y pieces beside da in dr
     unsigned dmask[WS], xmask[WS];  // bit i: piece i valid (else stored as zeros)
-    const HaloCol hc = halo_col(p.x, cc * CK + wg_piece(tid) * 8, p.dy);  // fixed for the whole block
+    const HaloCol hc = halo_col(p.x, cc * CK + wg_piece(tid) * 8, p.slab);  // fixed for the whole block (slab: any valid address)
     auto load_tile = [&](auto S, int tile) __attribute__((always_inline)) {
         const int tx = tile % p.tiles_x;
         const int rest = tile / p.tiles_x;
@@ -880,7 +921,9 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
             const int h = h0 + (rc >> 16), w = w0 + (rc & 0xffff);
             const bool ok = (rc >= 0) & (h < p.H) & (w < p.W);
             dm |= (unsigned)ok << i;
-            dr[S][i] = *reinterpret_cast<const uint4*>(p.dy + (ok ? (((size_t)b * p.H + h) * p.W + w) * p.M + mb + s * 8 : 0));
+            const size_t off = ok ? (((size_t)b * p.H + h) * p.W + w) * p.M + mb + s * 8 : 0;
+            dr[S][i] = *reinterpret_cast<const uint4*>((BNB ? p.bda : p.dy) + off);
+            if constexpr (BNB) yr[S][i] = *reinterpret_cast<const uint4*>(p.by + off);
         }
 #pragma unroll
         for (int i = 0; i < HP_PER_THREAD; ++i) {
@@ -894,11 +937,24 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
         xmask[S] = xm;
     };
     auto store_tile = [&](auto S) __attribute__((always_inline)) {
+        float ksc[BNB ? 8 : 1], ksh[BNB ? 8 : 1], kB[BNB ? 8 : 1], kC[BNB ? 8 : 1];
+        if constexpr (BNB) {  // the thread's dy piece is fixed: channels 8 * (tid % (COUT / 8)) + 0..7
+            const int c8 = (tid % (COUT / 8)) * 8;
+#pragma unroll
+            for (int h = 0; h < 8; h += 4) {
+                *reinterpret_cast<float4*>(ksc + h) = *reinterpret_cast<const float4*>(kbn + c8 + h);
+                *reinterpret_cast<float4*>(ksh + h) = *reinterpret_cast<const float4*>(kbn + COUT + c8 + h);
+                *reinterpret_cast<float4*>(kB + h) = *reinterpret_cast<const float4*>(kbn + 2 * COUT + c8 + h);
+                *reinterpret_cast<float4*>(kC + h) = *reinterpret_cast<const float4*>(kbn + 3 * COUT + c8 + h);
+            }
+        }
 #pragma unroll
         for (int i = 0; i < DY_PER_THREAD; ++i) {
             const int item = tid + i * 256;
             const int m = item / (COUT / 8), s = item - m * (COUT / 8);
-            *reinterpret_cast<uint4*>(dys + m * DY_LD + s * 8) = ((dmask[S] >> i) & 1u) ? dr[S][i] : make_uint4(0, 0, 0, 0);
+            uint4 v = dr[S][i];
+            if constexpr (BNB) v = bn_bwd_pk(v, yr[S][i], ksc, ksh, kB, kC);
+            *reinterpret_cast<uint4*>(dys + m * DY_LD + s * 8) = ((dmask[S] >> i) & 1u) ? v : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < HP_PER_THREAD; ++i) {  // every piece lands inside the HMAX-pixel region
@@ -949,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_halo_wgrad(const HWgArgs p) {
             for (int ks = 0; ks < ksteps; ++ks) kstep(ks);
         }
     };
-    if constexpr (COUT == 32) {
+    if constexpr (WS == 2) {
         // M = 32 (full-resolution layers, HBM-bound): two tiles in flight, unrolled by two so the
         // register-set index is static
         auto step = [&](auto S, int tile) __attribute__((always_inline)) {
@@ -1024,31 +1080,6 @@ constexpr int WS_PD = 5;                        // tap-steps of fragment read-ah
 // tiles carry little MFMA work and need more loads in flight; one otherwise
 __host__ __device__ constexpr int ws_blocks_per_cu(int cout, int cib) { return cout == 32 && cib == 32 ? 2 : 1; }
 
-// dy for 8 channels from the raw bf16 pieces (da, y): the BatchNorm-backward apply of k_bn_bwd_apply,
-// dy = k0*(dz - k1 - xhat*k2), dz = da where z = y*scale+shift > 0 (the forward ReLU mask, recomputed as
-// k_bn_bwd_apply does), xhat = (y-mean)*invstd, written in terms of z (which the mask needs anyway) with
-// k0 = scale: dy = scale*dz + Bz*z + Cz, Bz = -invstd*k2, Cz = invstd*k2*shift + scale*(mean*invstd*k2 - k1)
-__device__ __forceinline__ uint4 bn_bwd_pk(uint4 da, uint4 y, const float* sc, const float* sh, const float* Bz,
-                                           const float* Cz) {
-    const unsigned dw[4] = {da.x, da.y, da.z, da.w}, yw[4] = {y.x, y.y, y.z, y.w};
-    unsigned o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float r[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int c = 2 * i + h;
-            const float yv = __uint_as_float(h ? yw[i] & 0xffff0000u : yw[i] << 16);
-            const float dv = __uint_as_float(h ? dw[i] & 0xffff0000u : dw[i] << 16);
-            const float z = __builtin_fmaf(yv, sc[c], sh[c]);
-            const float t = __builtin_fmaf(Bz[c], z, Cz[c]);
-            r[h] = z > 0.f ? __builtin_fmaf(sc[c], dv, t) : t;
-        }
-        asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(o[i]) : "v"(r[0]), "v"(r[1]));
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
 template <int COUT, int CIB, int HP, int HR, bool BNB>  // dy / x channels per block; halo pitch and rows (tw+2 <= HP,
                                                        // th+2 <= HR); BNB: BatchNorm-backward apply in the dy staging
 __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_wgrad_ws(const HWgArgs p) {
@@ -1115,7 +1146,7 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
         const bool src1 = cc * CIB >= p.x.c0;
         const __bf16* xsrc = src1 ? p.x.p1 : p.x.p0;
         const int xC = src1 ? p.x.c1 : p.x.c0;
-        const HaloCol hc = halo_col(p.x, cc * CIB + xpiece * 8, p.dy);  // this thread's 8 channels (BN affine)
+        const HaloCol hc = halo_col(p.x, cc * CIB + xpiece * 8, p.slab);  // this thread's 8 channels (BN affine; slab: any valid address)
         // Per-piece element offsets from the tile origin (h0, w0), fixed for the launch: a piece's buffer
         // offset is then one add, its bounds test four compares against per-tile scalars, and a piece
         // outside the image / tile gets an offset past the buffer's range, which the buffer load returns
@@ -1219,8 +1250,8 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             if constexpr (BNB) {
                 // dy pieces outside the tile are zero (the raw pair loaded as zeros gives dy = C there); the
                 // writer block also stores them (buffer stores: out-of-range pieces dropped, no branch)
-                const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(
-                    (void*)(p.dy + (size_t)q.img * p.H * p.W * p.M), (short)0, p.H * p.W * p.M * 2, 0x00020000);
+                const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(  // no dy destination: 0 records
+                    (void*)(p.dy + (size_t)q.img * p.H * p.W * p.M), (short)0, p.dy ? p.H * p.W * p.M * 2 : 0, 0x00020000);
 #pragma unroll
                 for (int i = 0; i < DYP; ++i) {
                     const bool ok = (q.xm >> (16 + i)) & 1u;
@@ -1666,7 +1697,7 @@ int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
 const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W, bool bnb) {
     static thread_local char buf[64];
     const WsCfg ws = wgrad_ws(M, N, c0);
-    if (!ws.cib) return M == 32 ? "k_halo_wgrad<32>" : "k_halo_wgrad<64>";
+    if (!ws.cib) return M == 32 ? (bnb ? "k_halo_wgrad<32, true>" : "k_halo_wgrad<32, false>") : "k_halo_wgrad<64, false>";
     const WsTile t = wgrad_tile_ws(H, W);
     snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false");
     return buf;
@@ -1689,10 +1720,12 @@ static void launch_wgrad_ws(const WsCfg& ws, int hp, dim3 grid, hipStream_t st, 
 
 // the BatchNorm-backward apply fused into the dy staging: warp-specialised instances only. Returns the number
 // of x-channel blocks (grid.x) that each form the same dy tile (0: no fused kernel for the shape)
+// k_halo_wgrad<32, true> (x channels not a multiple of 32: enc1.0) only without a dy destination.
 int sd_halo_wgrad_bnbwd_blocks(const sd_src& a, const sd_src& b, int M, int N) {
     if (!sd_halo_wgrad_ok(a, b, M)) return 0;
     const WsCfg ws = wgrad_ws(M, N, b.chans[0]);
-    return ws.cib ? (N / 9) / ws.cib : 0;
+    if (ws.cib) return (N / 9) / ws.cib;
+    return M == 32 && !a.ptr[0] ? cdiv(b.chans[0] + b.chans[1], CK) : 0;
 }
 
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
@@ -1720,10 +1753,6 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
     p.bda = p.by = nullptr;
     p.bsc = p.bsh = p.bmu = p.bis = p.bcoef = nullptr;
     p.ncc = 1;
-    if (bnb && !ws.cib) {
-        sd_set_error("sd_wgrad_gemm_bnbwd: no fused kernel for M=%d N=%d", M, N);
-        return SD_EINVAL;
-    }
     if (bnb) {
         p.bda = (const __bf16*)bnb->da;
         p.by = (const __bf16*)bnb->y;
@@ -1746,10 +1775,16 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
     }
     p.xcd = halo_xcd_enabled() && (cdiv(p.x.ctot, CK) * splits * (M == 32 ? 1 : M / 64)) % 8 == 0;
     SD_REQUIRE(p.nhalo <= HMAX && t.th * t.tw <= WG_MAXPX, "sd_wgrad_gemm(halo): tile %dx%d", t.th, t.tw);
-    if (M == 32) {
-        hipLaunchKernelGGL(k_halo_wgrad<32>, dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
+    if (bnb) {  // enc1.0 (no dgrad): dy is not written
+        if (M != 32 || a.ptr[0]) {
+            sd_set_error("sd_wgrad_gemm_bnbwd: k_halo_wgrad fuses M = 32 without a dy destination only (M=%d)", M);
+            return SD_EINVAL;
+        }
+        hipLaunchKernelGGL((k_halo_wgrad<32, true>), dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
+    } else if (M == 32) {
+        hipLaunchKernelGGL((k_halo_wgrad<32, false>), dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
     } else {
-        hipLaunchKernelGGL(k_halo_wgrad<64>, dim3(cdiv(p.x.ctot, CK), splits, M / 64), dim3(256), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad<64, false>), dim3(cdiv(p.x.ctot, CK), splits, M / 64), dim3(256), 0, st, p);
     }
-    return sd_check_launch("sd_wgrad_gemm(halo)");
+    return sd_check_launch(bnb ? "sd_wgrad_gemm_bnbwd(halo)" : "sd_wgrad_gemm(halo)");
 }

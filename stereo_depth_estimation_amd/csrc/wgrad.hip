@@ -335,11 +335,14 @@ extern "C" int sd_wgrad_gemm_bnbwd(int dtype, const sd_src* a, const sd_src* b, 
                                    const void* da, const void* y, const float* scale, const float* shift,
                                    const float* mean, const float* invstd, const float* coef, float* slab, int splits,
                                    sd_stream s) {
-    if (int e = sd_validate_src(a, "sd_wgrad_gemm_bnbwd(a)")) return e;
+    SD_REQUIRE(a, "sd_wgrad_gemm_bnbwd: null a");
+    sd_src av = *a;  // a->ptr[0] may be NULL (dy not written): validate the shape with a stand-in pointer
+    if (!av.ptr[0]) av.ptr[0] = (const void*)16;
+    if (int e = sd_validate_src(&av, "sd_wgrad_gemm_bnbwd(a)")) return e;
     if (int e = sd_validate_src(b, "sd_wgrad_gemm_bnbwd(b)")) return e;
     SD_REQUIRE(dtype == SD_BF16, "sd_wgrad_gemm_bnbwd: bf16 only (dtype %d)", dtype);
     SD_REQUIRE(slab && splits > 0 && batch > 0 && H > 0 && W > 0, "sd_wgrad_gemm_bnbwd: bad args");
-    SD_REQUIRE(da && y && scale && shift && mean && invstd && coef && a->ptr[0], "sd_wgrad_gemm_bnbwd: null pointer");
+    SD_REQUIRE(da && y && scale && shift && mean && invstd && coef, "sd_wgrad_gemm_bnbwd: null pointer");
     SD_REQUIRE(a->taps == 1 && a->chans[0] == M && a->chans[1] == 0 && a->H == H && a->W == W && !a->scale[0],
                "sd_wgrad_gemm_bnbwd: A must be the plain 1x1 dy destination [pixels][M] on the grid");
     SD_REQUIRE(b->taps == 9 && b->H == H && b->W == W && (b->chans[0] + b->chans[1]) * 9 == N,

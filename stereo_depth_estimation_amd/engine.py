@@ -553,6 +553,10 @@ class UNetEngine:
         a = L.make_src(dy, cl.cout, Hl, Wl, taps=1)
         b = self._src_fwd(cl)
         M, N = cl.cout, 9 * cl.cin_pad
+        if not need_dgrad and dt == L.SD_BF16:  # enc1.0: nothing reads dy after the weight gradient
+            a_nody = L.make_src(None, cl.cout, Hl, Wl, taps=1)
+            if self.bn_fuse and L.call("sd_wgrad_bnbwd_ok", dt, a_nody, b, M, N) == 1:
+                a = a_nody
         # bf16: the weight gradient applies the BatchNorm backward while staging dy (and writes dy for the
         # dgrad), so the apply pass over (da, y) -> dy is gone; it runs first, the dgrad reads its dy. Each
         # x-channel block of the kernel repeats the transform of the same dy tile on its loader waves, whose VALU

@@ -85,7 +85,10 @@ def test_planning_queries_are_host_only():
     dy128 = L.make_src(ctypes.c_void_p(16), 128, 60, 80, taps=1)
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy128, x256, 128, 2304) == 4  # four 64-channel x blocks
     x8 = L.make_src(ctypes.c_void_p(16), 8, 240, 320, taps=9)
-    assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy, x8, 32, 72) == 0
+    assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy, x8, 32, 72) == 0  # enc1.0: only without a dy destination
+    nody = L.make_src(None, 32, 240, 320, taps=1)
+    assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, nody, x8, 32, 72) == 1
+    assert L.kernel_name("sd_wgrad_bnbwd_kernel_name", nody, x8, 32, 72) == "k_halo_wgrad<32, true>"
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_F32, dy, src, 32, 288) == 0
     # fp8 inference convs (live app, 960x720): one min/max row per persistent block
     assert L.call("sd_conv3x3_fp8_rows", 1, 720, 960, 32) == 256
@@ -97,7 +100,7 @@ def test_planning_queries_are_host_only():
 def test_fused_bn_wgrad_host_validation():
     dy = L.make_src(ctypes.c_void_p(16), 32, 24, 32, taps=1)
     x8 = L.make_src(ctypes.c_void_p(16), 8, 24, 32, taps=9)
-    with pytest.raises(L.StereoHipError, match="no fused kernel"):
+    with pytest.raises(L.StereoHipError, match="no fused kernel"):  # 8-channel x with a dy destination
         L.call("sd_wgrad_gemm_bnbwd", L.SD_BF16, dy, x8, 1, 24, 32, 32, 72, 1, 1, 1, 1, 1, 1, 1, 1, 1, None)
     x = L.make_src(ctypes.c_void_p(16), 32, 24, 32, taps=9)
     with pytest.raises(L.StereoHipError, match="bf16 only"):
