@@ -36,7 +36,7 @@ enum { SD_F32 = 0, SD_BF16 = 1 };
 /* gather transforms: identity, max(scale*x + shift, 0), scale*x + shift (fp8 quantisation of a signed source) */
 enum { SD_IDENT = 0, SD_BNRELU = 1, SD_AFFINE = 2 };
 /* conv-GEMM epilogues */
-enum { SD_EPI_STORE = 0, SD_EPI_STATS = 1, SD_EPI_SPLIT = 2, SD_EPI_PIXSHUF = 3 };
+enum { SD_EPI_STORE = 0, SD_EPI_STATS = 1, SD_EPI_SPLIT = 2, SD_EPI_PIXSHUF = 3, SD_EPI_SPLIT_STATS = 4 };
 /* weight-gradient layouts */
 enum { SD_W_CONV3 = 0, SD_W_CONVT = 1 };
 /* heads modes */
@@ -98,7 +98,10 @@ int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, void* out, sd
  * epi SD_EPI_STORE  : out0 NHWC [M][N]
  *     SD_EPI_STATS  : as STORE + stats[rows][N] float2 (sum, sumsq) per M-block (BN batch stats)
  *     SD_EPI_SPLIT  : n < n_split -> out0 [M][n_split], else out1 [M][N-n_split]  (cat backward)
- *     SD_EPI_PIXSHUF: n = t*C + o -> out0 [b][2h+t/2][2w+t%2][o] + bias[o]  (ConvTranspose2d) */
+ *     SD_EPI_PIXSHUF: n = t*C + o -> out0 [b][2h+t/2][2w+t%2][o] + bias[o]  (ConvTranspose2d)
+ *     SD_EPI_SPLIT_STATS: SPLIT + stats rows over all N columns (bf16, 3x3 halo shapes only): the dgrad of a
+ *                    decoder conv0 also yields the column sums of d(up), the ConvTranspose2d bias gradient
+ *                    (sd_stat_rows_sum) */
 int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi,
                  void* out0, void* out1, int n_split, const float* bias, float* stats, sd_stream s);
 /* number of float2 stat rows sd_conv_gemm(SD_EPI_STATS) writes for this shape */
@@ -167,6 +170,9 @@ int sd_bnrelu_pool(int dtype, const void* y, const float* scale, const float* sh
                    void* out, sd_stream s);
 /* column sums over pixels (ConvTranspose2d bias grad): partials then out[C] = sum (fp32) */
 int sd_chan_sum(int dtype, const void* x, int64_t pixels, int C, float* partials, float* out, sd_stream s);
+/* out[c] = sum over rows of stats[r][c].sum (float2 rows of ld columns, c < C; fp64 accumulation): the column
+ * sums of an SD_EPI_SPLIT_STATS (or STATS) launch, e.g. the ConvTranspose2d bias gradient (model.py:67-73) */
+int sd_stat_rows_sum(const float* stats, int rows, int ld, int C, float* out, sd_stream s);
 
 /* ---- heads + loss (model.py:76-77,98,103; train.py:329-356) ----
  * act = max(scale*y + shift, 0) [pixels][C] (dec1 output), head weights wd/wl [C], biases bd/bl [1].

@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("SD_HIP_LIB") or Path(__file__).resolve().parent 
 
 SD_F32, SD_BF16 = 0, 1
 SD_IDENT, SD_BNRELU, SD_AFFINE = 0, 1, 2
-SD_EPI_STORE, SD_EPI_STATS, SD_EPI_SPLIT, SD_EPI_PIXSHUF = 0, 1, 2, 3
+SD_EPI_STORE, SD_EPI_STATS, SD_EPI_SPLIT, SD_EPI_PIXSHUF, SD_EPI_SPLIT_STATS = 0, 1, 2, 3, 4
 SD_W_CONV3, SD_W_CONVT = 0, 1
 SD_HEADS_INFER, SD_HEADS_LOSS, SD_HEADS_GRADS = 0, 1, 2
 
@@ -115,6 +115,7 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_pool_bwd_rows": (_i, [_i, _i, _i, _i]),
     "sd_bnrelu_pool": (_i, [_i, _p, _p, _p, _i, _i, _i, _i, _p, _p]),
     "sd_chan_sum": (_i, [_i, _p, _i64, _i, _p, _p, _p]),
+    "sd_stat_rows_sum": (_i, [_p, _i, _i, _i, _p, _p]),
     "sd_count_valid": (_i, [_p, _p, _i64, _p, _p]),
     "sd_heads_rows": (_i, [_i64]),
     "sd_heads": (_i, [_i, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),

@@ -163,10 +163,10 @@ __global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restric
     }
 }
 
-__global__ __launch_bounds__(256) void k_sum_finalize(const float2* __restrict__ part, int rows, int C, float* out) {
+__global__ __launch_bounds__(256) void k_sum_finalize(const float2* __restrict__ part, int rows, int ld, float* out) {
     const int c = blockIdx.x;
     double s = 0.0, ss = 0.0;
-    for (int r = threadIdx.x; r < rows; r += 256) s += part[(size_t)r * C + c].x;
+    for (int r = threadIdx.x; r < rows; r += 256) s += part[(size_t)r * ld + c].x;
     block_sum2<256>(s, ss);
     if (threadIdx.x == 0) out[c] = (float)s;
 }
@@ -445,4 +445,10 @@ extern "C" int sd_chan_sum(int dtype, const void* x, int64_t pixels, int C, floa
     if (int e = sd_check_launch("sd_chan_sum")) return e;
     hipLaunchKernelGGL(k_sum_finalize, dim3(C), dim3(256), 0, to_stream(s), (const float2*)partials, rows, C, out);
     return sd_check_launch("sd_chan_sum(finalize)");
+}
+
+extern "C" int sd_stat_rows_sum(const float* stats, int rows, int ld, int C, float* out, sd_stream s) {
+    SD_REQUIRE(stats && out && rows > 0 && C > 0 && C <= ld, "sd_stat_rows_sum: bad args");
+    hipLaunchKernelGGL(k_sum_finalize, dim3(C), dim3(256), 0, to_stream(s), (const float2*)stats, rows, ld, out);
+    return sd_check_launch("sd_stat_rows_sum");
 }

@@ -321,15 +321,20 @@ extern "C" int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W,
         SD_REQUIRE(g.Hl == 2 * H && g.Wl == 2 * W, "sd_conv_gemm: sub-pixel source must be 2x the grid");
     else
         SD_REQUIRE(g.Hl == H && g.Wl == W, "sd_conv_gemm: source grid %dx%d != GEMM grid %dx%d", g.Hl, g.Wl, H, W);
-    SD_REQUIRE(epi >= SD_EPI_STORE && epi <= SD_EPI_PIXSHUF, "sd_conv_gemm: epi %d", epi);
-    if (epi == SD_EPI_STATS) SD_REQUIRE(stats != nullptr, "sd_conv_gemm: STATS needs stats buffer");
-    if (epi == SD_EPI_SPLIT)
+    SD_REQUIRE(epi >= SD_EPI_STORE && epi <= SD_EPI_SPLIT_STATS, "sd_conv_gemm: epi %d", epi);
+    if (epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS)
+        SD_REQUIRE(stats != nullptr, "sd_conv_gemm: STATS needs stats buffer");
+    if (epi == SD_EPI_SPLIT || epi == SD_EPI_SPLIT_STATS)
         SD_REQUIRE(out1 && n_split > 0 && n_split < N, "sd_conv_gemm: SPLIT needs out1 and 0<n_split<N");
+    if (epi == SD_EPI_SPLIT_STATS)
+        SD_REQUIRE(dtype == SD_BF16 && sd_halo_fwd_ok(*a, N, epi),
+                   "sd_conv_gemm: SPLIT_STATS is the bf16 3x3 halo epilogue (N = 32 or N %% 64 == 0)");
     if (epi == SD_EPI_PIXSHUF) SD_REQUIRE(bias && N % 4 == 0, "sd_conv_gemm: PIXSHUF needs bias and N%%4==0");
     const long long M = (long long)batch * H * W;
     SD_REQUIRE(M < (1LL << 31), "sd_conv_gemm: M too large");
     if (dtype == SD_BF16)  // bf16 epilogues store whole 8-channel (16-B) pieces
-        SD_REQUIRE(N % 8 == 0 && (epi != SD_EPI_SPLIT || n_split % 8 == 0) && (epi != SD_EPI_PIXSHUF || N % 32 == 0),
+        SD_REQUIRE(N % 8 == 0 && ((epi != SD_EPI_SPLIT && epi != SD_EPI_SPLIT_STATS) || n_split % 8 == 0) &&
+                       (epi != SD_EPI_PIXSHUF || N % 32 == 0),
                    "sd_conv_gemm: bf16 needs N (and n_split, N/4 for PIXSHUF) multiples of 8");
     if (dtype == SD_BF16 && epi == SD_EPI_STATS && sd_halo_fwd_shape(N))
         SD_REQUIRE(sd_halo_fwd_ok(*a, N, epi), "sd_conv_gemm: bf16 STATS with N=%d needs a 3x3 unpooled source", N);

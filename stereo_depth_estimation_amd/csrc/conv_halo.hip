@@ -649,7 +649,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const int ty = tl / p.tiles_x;
             const int h0 = ty * p.th, w0 = (tl - ty * p.tiles_x) * p.tw;
             const int hw_img = p.H * p.W;
-            const bool split = !STATS && p.epi == SD_EPI_SPLIT;  // STATS launches never split
+            const bool split = p.epi == SD_EPI_SPLIT || p.epi == SD_EPI_SPLIT_STATS;
             const int ns = split ? p.n_split : p.N;
             const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.out0 + (size_t)b * hw_img * ns), (short)0, hw_img * ns * 2, 0x00020000);
@@ -1525,7 +1525,7 @@ static HTile fwd_tile(int ctot, int H, int W, int N, bool stats) {
 
 const char* sd_halo_fwd_name(int H, int W, int N, int epi, int ctot) {
     static thread_local char buf[64];
-    const bool stats = epi == SD_EPI_STATS;
+    const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(ctot, H, W, N, stats);
     snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck, stats ? "true" : "false");
     return buf;
@@ -1548,7 +1548,7 @@ static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, cons
 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st) {
-    const bool st_ = epi == SD_EPI_STATS;
+    const bool st_ = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_);
     HFwdArgs p;
     p.a = make_halo_src(a);

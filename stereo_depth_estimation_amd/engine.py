@@ -154,6 +154,8 @@ class UNetEngine:
         self.ws: Workspace | None = None
         # bf16 training: BatchNorm-backward apply fused into the weight gradients (SD_BN_FUSE=0: separate pass)
         self.bn_fuse = os.environ.get("SD_BN_FUSE", "1") != "0"
+        # bf16 training: ConvTranspose2d bias gradients from the decoder dgrad epilogue (SD_BIAS_FUSE=0: own pass)
+        self.bias_fuse = os.environ.get("SD_BIAS_FUSE", "1") != "0"
         self.params: dict[str, torch.Tensor] = {}
         self.grads: dict[str, torch.Tensor] = {}
         self.bufs: dict[str, torch.Tensor] = {}
@@ -242,6 +244,9 @@ class UNetEngine:
                 t[f"{k}:{cl.name}"] = torch.empty(cl.cout, dtype=f32, device=dev)
             rows = L.call("sd_conv_gemm_stat_rows", dt, B, H >> cl.level, W >> cl.level, cl.cout)
             max_stat = max(max_stat, rows * cl.cout * 2)
+            if train and cl.blk in UP_OF_DEC and cl.idx == 0:  # dgrad SPLIT_STATS rows (ConvTranspose bias grad)
+                rows = L.call("sd_conv_gemm_stat_rows", dt, B, H >> cl.level, W >> cl.level, cl.cin)
+                max_stat = max(max_stat, rows * cl.cin * 2)
         t["stats"] = torch.empty(max_stat, dtype=f32, device=dev)
         for u in self.ups.values():
             t["u:" + u.name] = act(u.level - 1, u.cout)
@@ -585,8 +590,12 @@ class UNetEngine:
                        out.data_ptr(), None, 0, None, None, s)
             else:  # decoder: split into d(up) and d(skip) (cat backward, model.py:89-95)
                 up = self.ups[UP_OF_DEC[cl.blk]]
-                L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d, L.SD_EPI_SPLIT,
-                       t["du:" + up.name].data_ptr(), t["dskip:" + up.name].data_ptr(), up.cout, None, None, s)
+                # bf16: the same epilogue sums d(up) per channel = the ConvTranspose2d bias gradient (_up_bwd)
+                sums = self.bias_fuse and dt == L.SD_BF16 and (cl.cin == 32 or cl.cin % 64 == 0)
+                L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d,
+                       L.SD_EPI_SPLIT_STATS if sums else L.SD_EPI_SPLIT, t["du:" + up.name].data_ptr(),
+                       t["dskip:" + up.name].data_ptr(), up.cout, None, t["stats"].data_ptr() if sums else None, s)
+                self._up_bias_rows = (L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cin), cl.cin) if sums else None
         if not fuse:
             self._wgrad(a, b, cl.level, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key])
 
@@ -596,7 +605,14 @@ class UNetEngine:
         Hh, Wh = ws.H >> (u.level - 1), ws.W >> (u.level - 1)
         Hl, Wl = ws.H >> u.level, ws.W >> u.level
         P = ws.B * Hh * Wh
-        L.call("sd_chan_sum", dt, du.data_ptr(), P, u.cout, t["chan"].data_ptr(), self.grads[u.name + ".bias"].data_ptr(), s)
+        rows_ld = getattr(self, "_up_bias_rows", None)
+        if rows_ld is not None:  # left in t["stats"] by the decoder dgrad that produced du (_conv_bwd)
+            L.call("sd_stat_rows_sum", t["stats"].data_ptr(), rows_ld[0], rows_ld[1], u.cout,
+                   self.grads[u.name + ".bias"].data_ptr(), s)
+            self._up_bias_rows = None
+        else:
+            L.call("sd_chan_sum", dt, du.data_ptr(), P, u.cout, t["chan"].data_ptr(),
+                   self.grads[u.name + ".bias"].data_ptr(), s)
         src_cl = self.convs[UP_SRC[u.name] + ".1"]
         a = L.make_src(t["y:" + src_cl.name], src_cl.cout, Hl, Wl, taps=1, bn0=self._bn(src_cl))
         b = L.make_src(du, u.cout, Hh, Wh, taps=4)

@@ -150,6 +150,19 @@ def test_conv3x3_dual_source_and_dgrad_split(prec, B, H, W, c0, c1, co):
     gx = x.grad
     assert float((_from_nhwc(du, B, H, W, c0) - gx[:, :c0]).abs().max()) <= _tol(gx, prec)
     assert float((_from_nhwc(ds, B, H, W, c1) - gx[:, c0:]).abs().max()) <= _tol(gx, prec)
+    N = c0 + c1
+    if prec == "bf16" and (N == 32 or N % 64 == 0):
+        # SPLIT_STATS: the same stores, plus per-column sums of the stored values (ConvTranspose bias gradient)
+        du2, ds2 = torch.empty_like(du), torch.empty_like(ds)
+        rows = lib.call("sd_conv_gemm_stat_rows", lib.SD_BF16, B, H, W, N)
+        st = torch.empty(rows, N, 2, device=DEV)
+        lib.call("sd_conv_gemm", lib.SD_BF16, dsrc, B, H, W, wd.data_ptr(), N, kpd, lib.SD_EPI_SPLIT_STATS,
+                 du2.data_ptr(), ds2.data_ptr(), c0, None, st.data_ptr(), lib.stream_handle())
+        assert torch.equal(du2, du) and torch.equal(ds2, ds)
+        bias_grad = torch.empty(c0, device=DEV)
+        lib.call("sd_stat_rows_sum", st.data_ptr(), rows, N, c0, bias_grad.data_ptr(), lib.stream_handle())
+        ref_sum = du.double().sum(0).float()
+        assert torch.allclose(bias_grad, ref_sum, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
