@@ -275,7 +275,7 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
 bool sd_halo_fwd_ok(const sd_src& a, int N, int epi);
 bool sd_halo_fwd_shape(int N);
 int sd_halo_fwd_rows(int batch, int H, int W, int N);
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int ctot);
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1);
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st);
 
@@ -287,7 +287,7 @@ int sd_convt_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, in
 extern "C" const char* sd_conv_gemm_kernel_name(int dtype, const sd_src* a, int batch, int H, int W, int N, int epi) {
     static thread_local char buf[96];
     const long long M = (long long)batch * H * W;
-    if (dtype == SD_BF16 && a && sd_halo_fwd_ok(*a, N, epi)) return sd_halo_fwd_name(H, W, N, epi, a->chans[0] + a->chans[1]);
+    if (dtype == SD_BF16 && a && sd_halo_fwd_ok(*a, N, epi)) return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1]);
     if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, N, epi)) return sd_convt_fwd_name(*a);
     if (dtype == SD_BF16 && a && !a->pool) return sd_fast_fwd_name(M, N);
     const Cfg c = pick_cfg(M, N);

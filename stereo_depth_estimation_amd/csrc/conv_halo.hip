@@ -1523,11 +1523,15 @@ static HTile fwd_tile(int ctot, int H, int W, int N, bool stats) {
     return t;
 }
 
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int ctot) {
+// the instance as rocprofv3 names it: k_halo_conv<NT, RT, CK, STATS, WCONST> (launch_halo's choice)
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1) {
     static thread_local char buf[64];
     const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
-    const HTile t = fwd_tile(ctot, H, W, N, stats);
-    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck, stats ? "true" : "false");
+    const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
+    const bool wc = cdiv(c0, t.ck) + cdiv(c1, t.ck) == 1;
+    const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
+    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s>", N == 32 ? 1 : 2, t.rt, t.ck, stats ? "true" : "false",
+             wconst ? "true" : "false");
     return buf;
 }
 
