@@ -230,16 +230,20 @@ __device__ __forceinline__ int ld_pixel(int item) { return (item / (8 * PPX)) * 
 template <int PPX>
 __device__ __forceinline__ int ld_piece(int item) { return (item >> 3) % PPX; }
 
-template <int NT, int RT, int CK, bool STATS, bool WCONST>
+// IT items (spatial tiles of the same N-block) per pass: every chunk's weights are staged once for IT halos and
+// the MFMA waves keep IT accumulator sets (IT = 2 with CK = 16 halves the weight staging per MFMA)
+template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     constexpr int BN = 32 * NT;
     constexpr int PPX = CK / 8;                          // 16-B pieces per pixel (and per tap of a weight row)
     constexpr int HX_LD = halo_ld(CK), W_LD = wrow_ld(CK);
-    constexpr int HPX = halo_px_cap(RT, CK);
+    constexpr int HPX = IT == 2 ? 384 : halo_px_cap(RT, CK);  // IT = 2: the CK = 32 tilings (halo <= 384 px)
     constexpr int HP = (HPX * PPX + 255) / 256;          // halo pieces per loader thread
     constexpr int WPIECES = BN * 9 * PPX;                // weight pieces per chunk
     constexpr int W_PER_THREAD = (WPIECES + 255) / 256;
-    constexpr int HALO_ELEMS = HP * 256 / PPX * HX_LD, W_ELEMS = BN * W_LD, BUF = HALO_ELEMS + W_ELEMS;
+    constexpr int HALO_ITEM = HP * 256 / PPX * HX_LD;    // one item's halo region
+    constexpr int HALO_ELEMS = IT * HALO_ITEM, W_ELEMS = BN * W_LD, BUF = HALO_ELEMS + W_ELEMS;
+    static_assert(IT == 1 || (IT == 2 && HP * IT <= 16), "item masks fit 16 bits");
     constexpr int KS = (9 * CK + 15) / 16;               // 16-deep k-steps per chunk (CK 8: 5, the last half padding)
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
     // epilogue transpose scratch: 32 pixels x BN channels per MFMA wave (its own region, no block sync)
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     const int nchunks = nc0 + (p.a.c1 + CK - 1) / CK;
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
-    const int total = my_items * nchunks;            // chunk iterations (block-uniform)
+    const int total = (my_items + IT - 1) / IT * nchunks;  // chunk iterations (block-uniform), IT items each
     constexpr int LS = NT == 1 && CK == 8 ? 4 : 2;   // loader register sets (chunks in flight)
     const int padded = (total + LS - 1) / LS * LS;   // loader iterations
 
@@ -297,24 +301,28 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const int hy = px / p.hw;
             pgeo[i] = px < p.nhalo ? ((unsigned)hy << 16) | (unsigned)(px - hy * p.hw) : 0xffffffffu;
         }
-        int hpx[HP];  // image-local pixel of each piece for item ld_item, -1 outside the image
-        const __bf16* ib0 = p.a.p0;  // the item's image in source 0 / source 1
-        const __bf16* ib1 = p.a.p1;
-        int ld_item = 0, ld_cc = 0;
+        int hpx[IT][HP];  // image-local pixel of each piece for the items of pass ld_pass, -1 outside the image
+        const __bf16* ib0[IT];  // the items' images in source 0 / source 1
+        const __bf16* ib1[IT];
+        int ld_pass = 0, ld_cc = 0;
         auto geometry = [&]() __attribute__((always_inline)) {
-            // past the block's last item (unconditional loads): every piece out of range, no traffic
-            const bool live = ld_item < my_items;
-            const int sp = slot + ld_item * p.gper;
-            const int b = sp / p.tiles, tl = sp - b * p.tiles;
-            const int ty = tl / p.tiles_x;
-            const int h0 = ty * p.th - 1, w0 = (tl - ty * p.tiles_x) * p.tw - 1;
-            ib0 = p.a.p0 + (size_t)b * hw_img * p.a.c0;
-            ib1 = p.a.c1 ? p.a.p1 + (size_t)b * hw_img * p.a.c1 : p.a.p0;
 #pragma unroll
-            for (int i = 0; i < HP; ++i) {
-                const int h = h0 + (int)(pgeo[i] >> 16), w = w0 + (int)(pgeo[i] & 0xffffu);
-                const bool in = live & (pgeo[i] != 0xffffffffu) & (h >= 0) & (w >= 0) & (h < p.H) & (w < p.W);
-                hpx[i] = in ? h * p.W + w : -1;
+            for (int u = 0; u < IT; ++u) {
+                // past the block's last item (unconditional loads): every piece out of range, no traffic
+                const int itm = ld_pass * IT + u;
+                const bool live = itm < my_items;
+                const int sp = slot + (live ? itm : 0) * p.gper;
+                const int b = sp / p.tiles, tl = sp - b * p.tiles;
+                const int ty = tl / p.tiles_x;
+                const int h0 = ty * p.th - 1, w0 = (tl - ty * p.tiles_x) * p.tw - 1;
+                ib0[u] = p.a.p0 + (size_t)b * hw_img * p.a.c0;
+                ib1[u] = p.a.c1 ? p.a.p1 + (size_t)b * hw_img * p.a.c1 : p.a.p0;
+#pragma unroll
+                for (int i = 0; i < HP; ++i) {
+                    const int h = h0 + (int)(pgeo[i] >> 16), w = w0 + (int)(pgeo[i] & 0xffffu);
+                    const bool in = live & (pgeo[i] != 0xffffffffu) & (h >= 0) & (w >= 0) & (h < p.H) & (w < p.W);
+                    hpx[u][i] = in ? h * p.W + w : -1;
+                }
             }
         };
         // weights: byte offset of each piece in chunk 0 (OOB: past the weight rows of this N-block)
@@ -343,8 +351,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         static_assert(LS == 2 || LS == 4, "set (g % LS) and buffer (g & 1) static per unrolled iteration");
         // one object per set (an array of sets past ~256 B stays in scratch instead of registers)
         struct HSet {
-            uint4 hr[HP];
-            unsigned m;  // bit i: piece i inside the image (and the channels)
+            uint4 hr[IT][HP];
+            unsigned m;  // bit u*HP + i: piece i of item u inside the image (and the channels)
             int cb;      // the chunk's first channel (BN affine index)
             bool bn;     // BN+ReLU source
         };
@@ -400,27 +408,30 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const bool cok = cl + lpiece * 8 < C;
             // one buffer load per piece on the source's image; pieces outside the image or past the source's
             // channels are out of range (zeros; masked again after a BN transform)
-            const __amdgpu_buffer_rsrc_t hrs =
-                __builtin_amdgcn_make_buffer_rsrc((void*)(s1 ? ib1 : ib0), (short)0, hw_img * C * 2, 0x00020000);
             unsigned m = 0;
 #pragma unroll
-            for (int i = 0; i < HP; ++i) {
-                const bool ok = (hpx[i] >= 0) & cok;
-                m |= (unsigned)ok << i;
-                unsigned off;
-                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(hpx[i]), "s"(C * 2), "v"(lpiece * 16));
-                off = ok ? off : OOB;
-                if (WG_EXP & 262144) {
-                    q.hr[i] = make_uint4(off, off, off, off);
-                    continue;
+            for (int u = 0; u < IT; ++u) {
+                const __amdgpu_buffer_rsrc_t hrs =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)(s1 ? ib1[u] : ib0[u]), (short)0, hw_img * C * 2, 0x00020000);
+#pragma unroll
+                for (int i = 0; i < HP; ++i) {
+                    const bool ok = (hpx[u][i] >= 0) & cok;
+                    m |= (unsigned)ok << (u * HP + i);
+                    unsigned off;
+                    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(hpx[u][i]), "s"(C * 2), "v"(lpiece * 16));
+                    off = ok ? off : OOB;
+                    if (WG_EXP & 262144) {
+                        q.hr[u][i] = make_uint4(off, off, off, off);
+                        continue;
+                    }
+                    const auto x = __builtin_amdgcn_raw_buffer_load_b128(hrs, off, cl * 2, 0);
+                    q.hr[u][i] = make_uint4(x[0], x[1], x[2], x[3]);
                 }
-                const auto x = __builtin_amdgcn_raw_buffer_load_b128(hrs, off, cl * 2, 0);
-                q.hr[i] = make_uint4(x[0], x[1], x[2], x[3]);
             }
             q.m = m;
             if (++ld_cc == nchunks) {
                 ld_cc = 0;
-                ++ld_item;
+                ++ld_pass;
                 geometry();
             }
         };
@@ -437,15 +448,17 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             }
             if (!(WG_EXP & 32))
 #pragma unroll
-            for (int i = 0; i < HP; ++i) {  // every piece lands inside the halo region
+            for (int u = 0; u < IT; ++u)
+#pragma unroll
+            for (int i = 0; i < HP; ++i) {  // every piece lands inside the item's halo region
                 const int item = ltid + i * 256;
-                uint4 v = q.hr[i];
-                const bool ok = (q.m >> i) & 1u;
+                uint4 v = q.hr[u][i];
+                const bool ok = (q.m >> (u * HP + i)) & 1u;
                 if (q.bn && !(WG_EXP & 2048)) {
                     v = bnrelu_pk(v, s0, s1, h0, h1);
                     v = ok ? v : make_uint4(0, 0, 0, 0);  // zero padding after the activation
                 }
-                *reinterpret_cast<uint4*>(hx + ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8) = v;
+                *reinterpret_cast<uint4*>(hx + u * HALO_ITEM + ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8) = v;
             }
             if constexpr (!WCONST) if (!(WG_EXP & 131072)) store_w(buf);
         };
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     float own[NOWN];  // [q*2 + {sum, sumsq}] of channel n0 + 8*(lane % PPP) + q
 #pragma unroll
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
-    f32x16 acc[RT][NT];
+    f32x16 acc[IT][RT][NT];
     // Epilogue: the bf16 results go through this wave's LDS scratch (pixel rows of BN channels, 16-B pieces
     // XOR-swizzled by pixel so both the row-per-lane writes and the piece-per-lane reads are conflict-free)
     // and leave as stores of EPR whole pixels per instruction (1 KiB contiguous, 8 or 16 full 128-B lines)
@@ -566,7 +579,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 
     constexpr bool DG = (WG_EXP & 1024) != 0;
     unsigned long long t_cp = 0, t_ep = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
-    int cc = 0, item = 0;
+    int cc = 0, pass = 0;
     for (int gi = 0; gi < total; ++gi) {
         if (DG) t0 = __builtin_amdgcn_s_memtime();
         if (WG_EXP & 16384) {
@@ -585,11 +598,13 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         }
         if (cc == 0) {
 #pragma unroll
+            for (int u = 0; u < IT; ++u)
+#pragma unroll
             for (int i = 0; i < RT; ++i)
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
+                    for (int r = 0; r < 16; ++r) acc[u][i][t][r] = 0.f;
         }
         const __bf16* hx = smem + (gi & 1) * BUF;
         const __bf16* wl = hx + HALO_ELEMS;
@@ -599,7 +614,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #define HC_PF 1
 #endif
         constexpr int PF = HC_PF;
-        bf16x8 af[PF + 1][RT], bfr[PF + 1][NT];
+        bf16x8 af[PF + 1][IT][RT], bfr[PF + 1][NT];
         auto read_frags = [&](int step) {
             const int slot_ = step % (PF + 1);
             // CK 8: a k-step is two taps of 8 channels (lane half = tap parity); tap 9 is padding
@@ -613,8 +628,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 if (CK == 8 && tapv > 8) bfr[slot_][t] = bf16x8{};  // zero weights for the padding tap
             }
 #pragma unroll
+            for (int u = 0; u < IT; ++u)
+#pragma unroll
             for (int i = 0; i < RT; ++i)
-                af[slot_][i] = *reinterpret_cast<const bf16x8*>(hx + (abase[i] + toff) * HX_LD + c8 * 8);
+                af[slot_][u][i] = *reinterpret_cast<const bf16x8*>(hx + u * HALO_ITEM + (abase[i] + toff) * HX_LD + c8 * 8);
         };
         if (!(WG_EXP & 8)) {
 #pragma unroll
@@ -625,10 +642,12 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             __builtin_amdgcn_sched_barrier(0);
             const int sl = step % (PF + 1);
 #pragma unroll
+            for (int u = 0; u < IT; ++u)
+#pragma unroll
             for (int i = 0; i < RT; ++i)
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
-                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[sl][t], af[sl][i], acc[i][t], 0, 0, 0);
+                    acc[u][i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[sl][t], af[sl][u][i], acc[u][i][t], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
         }
@@ -643,7 +662,11 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             __builtin_amdgcn_sched_barrier(0);
         }
         if (++cc == nchunks) {
-            // ---------------------------------------------------- epilogue of `item`
+#pragma unroll
+          for (int u = 0; u < IT; ++u) {
+            // ---------------------------------------------------- epilogue of the pass's item u
+            const int item = pass * IT + u;
+            if (IT > 1 && item >= my_items) break;  // the last pass's missing item (block-uniform)
             const int sp = slot + item * p.gper;
             const int b = sp / p.tiles, tl = sp - b * p.tiles;
             const int ty = tl / p.tiles_x;
@@ -665,7 +688,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     for (int g4 = 0; g4 < 4; ++g4) {
                         bf16x4 v;
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[i][t][4 * g4 + q];
+                        for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[u][i][t][4 * g4 + q];
                         pk[g4] = *reinterpret_cast<uint2*>(&v);
                     }
                     // lanes l and l+32 hold the two 4-channel halves of each 8-channel group of one pixel:
@@ -714,8 +737,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 }
                 asm volatile("" ::: "memory");  // the next tile's writes after these reads
             }
+          }
             cc = 0;
-            ++item;
+            ++pass;
             if (DG) {
                 const unsigned long long t1 = __builtin_amdgcn_s_memtime();
                 t_ep += t1 - t0;
@@ -1435,6 +1459,7 @@ static bool halo_xcd_enabled() {
 // wave (th*tw <= 128*RT), CK-channel chunks.
 struct HTile {
     int th, tw, rt, ck;
+    int it = 1;  // items per pass (k_halo_conv IT)
 };
 // per-CU cycles of one chunk: the MFMA pipe of one SIMD vs the LDS (fragment reads at 4 cycles per
 // ds_read_b128, staging stores at ~79 B/cycle: MI355X_MICROARCH.md LDS table)
@@ -1517,9 +1542,23 @@ int sd_halo_fwd_rows(int batch, int H, int W, int N) {
 
 // the tile plus its chunk width: 8-channel sources (the padded network input) with N = 32 take CK = 8
 // chunks (5 k-steps per tile instead of 18 over 24 zero channels), same tiles (and stat rows)
+// SD_HALO_IT=2: N % 64 layers with more than one 32-channel chunk run two items per pass at CK = 16 (each chunk's
+// weights staged once for two halos)
+static int halo_it_env() {
+    static const int v = [] {
+        const char* e = getenv("SD_HALO_IT");
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
 static HTile fwd_tile(int ctot, int H, int W, int N, bool stats) {
     HTile t = halo_tile(H, W, N, stats);
     if (ctot <= 8 && N == 32) t.ck = 8;
+    if (halo_it_env() == 2 && N % 64 == 0 && t.ck == 32 && ctot > 32 && t.rt == 2 &&
+        (t.th + 2) * (t.tw + 2) <= 384) {
+        t.ck = 16;
+        t.it = 2;
+    }
     return t;
 }
 
@@ -1530,24 +1569,24 @@ const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1) {
     const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
     const bool wc = cdiv(c0, t.ck) + cdiv(c1, t.ck) == 1;
     const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
-    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s>", N == 32 ? 1 : 2, t.rt, t.ck, stats ? "true" : "false",
-             wconst ? "true" : "false");
+    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d>", N == 32 ? 1 : 2, t.rt, t.ck,
+             stats ? "true" : "false", wconst ? "true" : "false", t.it);
     return buf;
 }
 
 // wconst (one chunk per item): the weights are staged once per block. CK = 8 always has one chunk; CK = 16
 // (experiments) always takes the general instance, which is also correct with one chunk.
-template <int NT, int RT, int CK>
+template <int NT, int RT, int CK, int IT = 1>
 static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p) {
     constexpr bool W0 = CK == 8, W1 = CK != 16;  // the instance for wconst false / true
     if (stats && (wconst ? W1 : W0))
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W1>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W1, IT>), grid, dim3(512), 0, st, p);
     else if (stats)
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W0>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W0, IT>), grid, dim3(512), 0, st, p);
     else if (wconst ? W1 : W0)
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1, IT>), grid, dim3(512), 0, st, p);
     else
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0, IT>), grid, dim3(512), 0, st, p);
 }
 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
@@ -1575,7 +1614,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.stats = stats;
     p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
     p.dbg = g_wg_dbg;
-    SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= halo_px_cap(t.rt, t.ck) && t.th * t.tw <= 128 * t.rt &&
+    SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= (t.it == 2 ? 384 : halo_px_cap(t.rt, t.ck)) && t.th * t.tw <= 128 * t.rt &&
                    t.th < 64 && t.tw < 512,
                "sd_conv_gemm(halo): tile %dx%d (RT %d, CK %d)", t.th, t.tw, t.rt, t.ck);
     SD_REQUIRE((long long)batch * p.tiles < (1LL << 30), "sd_conv_gemm(halo): too many tiles");
@@ -1597,6 +1636,8 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     } else if (t.ck == 32) {
         if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p);
         else launch_halo<2, 2, 32>(st_, wc, grid, st, p);
+    } else if (t.it == 2) {  // RT = 2 only (RT = 3 with two accumulator sets spills)
+        launch_halo<2, 2, 16, 2>(st_, wc, grid, st, p);
     } else if (t.rt == 4) {
         launch_halo<2, 4, 16>(st_, wc, grid, st, p);
     } else if (t.rt == 3) {
