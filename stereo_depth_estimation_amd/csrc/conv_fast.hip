@@ -539,9 +539,15 @@ struct FCfg {
     int bm, bn, wm, wn;
 };
 FCfg pick_fwd(long long M, int N) {
+    static const int bm_env = [] {  // SD_FWD_BM=128: 128-row tiles for N > 64 at large M (A/B runs)
+        const char* e = getenv("SD_FWD_BM");
+        return e ? atoi(e) : 0;
+    }();
     if (N <= 32) return {256, 32, 4, 1};
     if (N <= 64) return {128, 64, 2, 2};
-    if (M >= 128LL * 96) return {128, 128, 2, 2};
+    // 64-row tiles unless SD_FWD_BM=128: twice the blocks for the ConvTranspose dgrad / up4 GEMMs, whose blocks
+    // wait on one global round trip per K tile (measured: up4 dgrad 67 -> 54 us, up3 62 -> 57, up2 equal)
+    if (M >= 128LL * 96 && bm_env == 128) return {128, 128, 2, 2};
     return {64, 128, 2, 2};
 }
 FCfg pick_wg(int M, int N) {
@@ -571,9 +577,13 @@ const char* sd_fast_wgrad_name(int M, int N) {
 }
 
 int sd_fast_wgrad_splits(long long P, int M, int N) {
+    static const int target = [] {  // SD_FWG_BLOCKS: split-K blocks of the ConvTranspose weight gradients (A/B runs)
+        const char* e = getenv("SD_FWG_BLOCKS");
+        return e && atoi(e) > 0 ? atoi(e) : 512;  // one round at two blocks per CU (measured 9 us faster per layer than 1024)
+    }();
     const FCfg c = pick_wg(M, N);
     const long long tiles = (long long)cdiv(M, c.bm) * cdiv(N, c.bn);
-    long long splits = (1024 + tiles - 1) / tiles;
+    long long splits = (target + tiles - 1) / tiles;
     const long long max_splits = (P + 64 * 8 - 1) / (64 * 8);  // >= 8 K tiles per block
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
