@@ -74,13 +74,15 @@ class GemmTimer:
     def _flops_and_name(self, name, args):
         L, eng = self.L, self.eng
         xin = eng.ws.t["xin"].data_ptr()
-        if name == "sd_conv_gemm":
+        if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             dt, src, B, H, W, _, N = args[:7]
             s = src._obj if hasattr(src, "_obj") else src
             ctot = s.chans[0] + s.chans[1]
             if s.ptr[0] == xin:
                 ctot = eng.in_channels  # enc1.0: 6 real channels padded to 8
             flops = 2.0 * B * H * W * N * s.taps * ctot
+            if name == "sd_conv_gemm_bnsum":  # a dgrad (STORE) that also sums the BatchNorm backward
+                return flops, L.kernel_name("sd_conv_gemm_bnsum_kernel_name", s, H, W, N)
             return flops, L.kernel_name("sd_conv_gemm_kernel_name", dt, s, B, H, W, N, args[8])
         dt, a, b, B, H, W, M, N = args[:8]
         sb = b._obj if hasattr(b, "_obj") else b
@@ -92,7 +94,7 @@ class GemmTimer:
         return 2.0 * B * H * W * M * n_real, L.kernel_name("sd_wgrad_kernel_name", dt, a, sb, M, N)
 
     def __call__(self, name, args, phase):
-        if name not in ("sd_conv_gemm", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd"):
+        if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
         ev.record()
@@ -149,7 +151,7 @@ class GemmTimer:
 
     @staticmethod
     def _shape(name, args):
-        if name == "sd_conv_gemm":
+        if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             s = args[1]
             return f"fwd M={args[2] * args[3] * args[4]} N={args[6]} K={s.taps}x{s.chans[0] + s.chans[1]}"
         b = args[2]

@@ -110,6 +110,17 @@ int sd_conv_gemm_stat_rows(int dtype, int batch, int H, int W, int N);
 const char* sd_conv_gemm_kernel_name(int dtype, const sd_src* a, int batch, int H, int W, int N, int epi);
 const char* sd_wgrad_kernel_name(int dtype, const sd_src* a, const sd_src* b, int M, int N);
 
+/* sd_conv_gemm(SD_EPI_STORE) of a dgrad whose output `out` is the upstream gradient da of a BatchNorm layer with raw
+ * output y (model.py:37,40): the same launch also writes that layer's BatchNorm-backward partial sums (what
+ * sd_bn_bwd_reduce computes from da and y in a pass of its own), sd_conv_gemm_bnsum_rows() rows of float2[N],
+ * for sd_bn_bwd_finalize. bf16 3x3 halo shapes: sd_conv_gemm_bnsum_ok. */
+int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad,
+                       void* out, const void* y, const float* scale, const float* shift, const float* mean,
+                       const float* invstd, float* partials, sd_stream s);
+int sd_conv_gemm_bnsum_ok(int dtype, const sd_src* a, int N);
+int sd_conv_gemm_bnsum_rows(const sd_src* a, int batch, int H, int W, int N);
+const char* sd_conv_gemm_bnsum_kernel_name(const sd_src* a, int H, int W, int N);
+
 /* ---- weight gradient (replaces convolution_backward wgrad, model.py:36,39,67-73) ----
  * slab[z][m][n] = sum over the z-th pixel range of A(p, m) * B(p, n), p over batch x H x W. */
 int sd_wgrad_splits(int dtype, int batch, int H, int W, int M, int N);

@@ -27,6 +27,12 @@ int sd_check_launch(const char* what);
 
 static inline hipStream_t to_stream(sd_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// BatchNorm layer whose backward sums a dgrad epilogue accumulates (sd_conv_gemm_bnsum -> conv_halo.hip)
+struct HaloBnSum {
+    const void* y;
+    const float *scale, *shift, *mean, *invstd;
+};
+
 // BatchNorm-backward operands of the fused weight gradient (sd_wgrad_gemm_bnbwd -> conv_halo.hip)
 struct HaloBnBwd {
     const void* da;

@@ -275,9 +275,11 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
 bool sd_halo_fwd_ok(const sd_src& a, int N, int epi);
 bool sd_halo_fwd_shape(int N);
 int sd_halo_fwd_rows(int batch, int H, int W, int N);
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1);
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns = false);
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
-                     void* out1, int n_split, float* stats, hipStream_t st);
+                     void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns = nullptr);
+int sd_halo_store_rows(int batch, int H, int W, int N, int ctot);
+bool sd_halo_bnsum_ok(const sd_src& a, int N);
 
 bool sd_convt_fwd_ok(const sd_src& a, int N, int epi);
 const char* sd_convt_fwd_name(const sd_src& a);
@@ -355,4 +357,31 @@ extern "C" int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W,
     IgemmArgs<float> p{g, H, W, (int)M, (const float*)wpack, N, kpad, cdiv(g.kchunks, KC), epi,
                        (float*)out0, (float*)out1, n_split, bias, stats};
     return launch_igemm(p, to_stream(s));
+}
+
+extern "C" int sd_conv_gemm_bnsum_ok(int dtype, const sd_src* a, int N) {
+    return dtype == SD_BF16 && a && a->xform[0] != SD_AFFINE && a->xform[1] != SD_AFFINE && sd_halo_bnsum_ok(*a, N) ? 1 : 0;
+}
+
+extern "C" int sd_conv_gemm_bnsum_rows(const sd_src* a, int batch, int H, int W, int N) {
+    return a ? sd_halo_store_rows(batch, H, W, N, a->chans[0] + a->chans[1]) : 0;
+}
+
+extern "C" const char* sd_conv_gemm_bnsum_kernel_name(const sd_src* a, int H, int W, int N) {
+    if (!a || !sd_halo_bnsum_ok(*a, N)) return "";
+    return sd_halo_fwd_name(H, W, N, SD_EPI_STORE, a->chans[0], a->chans[1], true);
+}
+
+extern "C" int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N,
+                                  int kpad, void* out, const void* y, const float* scale, const float* shift,
+                                  const float* mean, const float* invstd, float* partials, sd_stream s) {
+    if (int e = validate_src(a, "sd_conv_gemm_bnsum")) return e;
+    SD_REQUIRE(sd_conv_gemm_bnsum_ok(dtype, a, N), "sd_conv_gemm_bnsum: bf16 CK = 32 halo shapes only (_ok)");
+    SD_REQUIRE(batch > 0 && H > 0 && W > 0 && wpack && out && y && scale && shift && mean && invstd && partials,
+               "sd_conv_gemm_bnsum: bad args");
+    GatherSrc g = make_gather(*a);
+    SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == H && g.Wl == W, "sd_conv_gemm_bnsum: kpad/grid");
+    const HaloBnSum bns{y, scale, shift, mean, invstd};
+    return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, SD_EPI_STORE, out, nullptr, 0, partials, to_stream(s),
+                            &bns);
 }

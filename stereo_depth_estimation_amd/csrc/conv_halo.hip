@@ -209,6 +209,11 @@ struct HFwdArgs {
     float* stats;         // [gper][N] float2 (sum, sumsq of the stored bf16 values)
     int xcd;              // 1: XCD-contiguous block numbering (grid % 8 == 0)
     unsigned long long* dbg;  // timing-diagnostic builds only (WG_EXP & 1024): per-wave cycle counters
+    // BNS (sd_conv_gemm_bnsum): the stored output is the upstream gradient da of a BatchNorm layer whose raw
+    // output is by; the stats rows get (sum dz, sum dz*xhat) of it, dz = da where by*scale+shift > 0,
+    // xhat = (by-mean)*invstd (what sd_bn_bwd_reduce computes in a pass of its own)
+    const __bf16* by;
+    const float *bsc, *bsh, *bmu, *bis;
 };
 
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
@@ -232,7 +237,7 @@ __device__ __forceinline__ int ld_piece(int item) { return (item >> 3) % PPX; }
 
 // IT items (spatial tiles of the same N-block) per pass: every chunk's weights are staged once for IT halos and
 // the MFMA waves keep IT accumulator sets (IT = 2 with CK = 16 halves the weight staging per MFMA)
-template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT>
+template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     constexpr int BN = 32 * NT;
     constexpr int PPX = CK / 8;                          // 16-B pieces per pixel (and per tap of a weight row)
@@ -546,8 +551,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // BN statistics of the stored values, taken from the transposed pieces: a lane always reads channels
     // n0 + 8*(lane % PPP) + 0..7, so it keeps 8 (sum, sumsq) pairs across all of the block's items and the
     // lanes sharing channels are reduced once at the end.
-    constexpr int NOWN = STATS ? 16 : 1;
-    float own[NOWN];  // [q*2 + {sum, sumsq}] of channel n0 + 8*(lane % PPP) + q
+    static_assert(!(STATS && BNS), "one kind of stats rows");
+    constexpr int NOWN = STATS || BNS ? 16 : 1;
+    float own[NOWN];  // [q*2 + {sum, sumsq}] of channel n0 + 8*(lane % PPP) + q; BNS: {sum dz, sum dz*xhat}
 #pragma unroll
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
     f32x16 acc[IT][RT][NT];
@@ -576,6 +582,41 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             erel[k / 2] = (erel[k / 2] & ~(0xffffu << (16 * (k & 1)))) | (v << (16 * (k & 1)));
         }
     __bf16* const scw = scr + wid * 32 * BN;
+    // BNS: the lane's 8 channels are fixed (piece lane % PPP): their BatchNorm constants in registers, and the y
+    // pieces of an item's stores prefetched while its last chunk is in the matrix core
+    constexpr int NBK = BNS ? 8 : 1, NYQ = BNS ? RT * ER : 1;
+    float bk_sc[NBK], bk_sh[NBK], bk_mu[NBK], bk_is[NBK];
+    uint4 yq[NYQ];
+    if constexpr (BNS) {
+        const int c = n0 + (lane % PPP) * 8;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bool cin = c + q < p.N;
+            bk_sc[q] = cin ? p.bsc[c + q] : 0.f;
+            bk_sh[q] = cin ? p.bsh[c + q] : 0.f;
+            bk_mu[q] = cin ? p.bmu[c + q] : 0.f;
+            bk_is[q] = cin ? p.bis[c + q] : 0.f;
+        }
+    }
+    auto prefetch_y = [&](int itm) __attribute__((always_inline)) {  // the y pieces this lane stores for item itm
+        const int sp = slot + itm * p.gper;
+        const int b = sp / p.tiles, tl = sp - b * p.tiles;
+        const int ty = tl / p.tiles_x;
+        const int h0 = ty * p.th, w0 = (tl - ty * p.tiles_x) * p.tw;
+        const int hw_img = p.H * p.W;
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.by + (size_t)b * hw_img * p.N), (short)0, hw_img * p.N * 2, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < RT * ER; ++k) {
+            const unsigned rel = (erel[k / 2] >> (16 * (k & 1))) & 0xffffu;
+            const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
+            const int c = n0 + (lane % PPP) * 8;
+            const bool in = (rel != 0xffffu) & (h < p.H) & (w < p.W) & (c < p.N);
+            const unsigned off = in ? (unsigned)((h * p.W + w) * p.N + c) * 2u : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+            yq[k] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
 
     constexpr bool DG = (WG_EXP & 1024) != 0;
     unsigned long long t_cp = 0, t_ep = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
@@ -605,6 +646,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 for (int t = 0; t < NT; ++t)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) acc[u][i][t][r] = 0.f;
+        }
+        if constexpr (BNS) {
+            if (cc == nchunks - 1) prefetch_y(pass);  // IT == 1: the pass is the item
         }
         const __bf16* hx = smem + (gi & 1) * BUF;
         const __bf16* wl = hx + HALO_ELEMS;
@@ -711,6 +755,23 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     const bool live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
                     const bool in = live & !(WG_EXP & 4096);
                     const int pix = h * p.W + w, c = n0 + j * 8;
+                    if constexpr (BNS) {
+                        const uint4 yv = yq[i * ER + r];
+                        const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                            for (int hh = 0; hh < 2; ++hh) {
+                                const int ch = 2 * q + hh;
+                                const float d = __uint_as_float(hh ? wv[q] & 0xffff0000u : wv[q] << 16);
+                                const float yy = __uint_as_float(hh ? yw[q] & 0xffff0000u : yw[q] << 16);
+                                const float z = __builtin_fmaf(yy, bk_sc[ch], bk_sh[ch]);
+                                const float dz = (live & (z > 0.f)) ? d : 0.f;
+                                own[4 * q + 2 * hh] += dz;
+                                own[4 * q + 2 * hh + 1] = __builtin_fmaf(dz, (yy - bk_mu[ch]) * bk_is[ch], own[4 * q + 2 * hh + 1]);
+                            }
+                        }
+                    }
                     if constexpr (STATS) {
                         const unsigned wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -757,7 +818,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     }
 
     // ---------------------------------------------------------------- BN statistics row
-    if constexpr (STATS) {
+    if constexpr (STATS || BNS) {
         // lanes l, l + PPP, l + 2*PPP, ... hold the same 8 channels (of different pixels)
 #pragma unroll
         for (int k = 0; k < NOWN; ++k) {
@@ -770,7 +831,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         }
     }
     __syncthreads();
-    if (STATS && tid < BN && n0 + tid < p.N) {
+    if ((STATS || BNS) && tid < BN && n0 + tid < p.N) {
         float s = 0.f, ss = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -1477,10 +1538,11 @@ static HTile halo_tile(int H, int W, int N, bool stats) {
     const char* env = getenv("SD_HALO_CK");
     const int ck = nt == 1 ? 32 : (env && atoi(env) == 16 ? 16 : 32);
     if (nt == 1 && W % 32 == 0 && H % 16 == 0) {
-        // full-res N=32: 16x32 tiles (RT 4), except 8x32 (RT 2) for the STATS epilogue, whose 16x32
-        // instance spills (measured 227 vs 282 us at 240x320x64); SD_HALO_N32=8/16 forces one (experiments)
+        // full-res N=32: 16x32 tiles (RT 4), also for the STATS epilogue since the r02 epilogue (no spill at
+        // RT 4: dec1.0 fwd 313 -> 278 us, enc1.0 127 -> 109 us against 8x32); SD_HALO_N32=8/16 forces one
         const char* e32 = getenv("SD_HALO_N32");
-        const int rows = e32 ? atoi(e32) : (stats ? 8 : 16);
+        const int rows = e32 ? atoi(e32) : 16;
+        (void)stats;
         return rows == 8 ? HTile{8, 32, 2, 32} : HTile{16, 32, 4, 32};
     }
     if (ck == 32) {  // 8x32, 6x40, a whole small image, rows of the image (<= 320 pixels, <= 384 halo)
@@ -1562,35 +1624,58 @@ static HTile fwd_tile(int ctot, int H, int W, int N, bool stats) {
     return t;
 }
 
+// partial rows of a STORE launch (sd_conv_gemm_bnsum): one per block of an N-block, like STATS
+int sd_halo_store_rows(int batch, int H, int W, int N, int ctot) {
+    int nblk, gper, nsp;
+    halo_grid(fwd_tile(ctot, H, W, N, false), batch, H, W, N, nblk, gper, nsp);
+    return gper;
+}
+bool sd_halo_bnsum_ok(const sd_src& a, int N) {
+    if (!sd_halo_fwd_ok(a, N, SD_EPI_STORE)) return false;
+    const HTile t = fwd_tile(a.chans[0] + a.chans[1], a.H, a.W, N, false);
+    return t.ck == 32 && t.it == 1 && !(N != 32 && t.rt == 3);
+}
+
 // the instance as rocprofv3 names it: k_halo_conv<NT, RT, CK, STATS, WCONST> (launch_halo's choice)
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1) {
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns) {
     static thread_local char buf[64];
     const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
     const bool wc = cdiv(c0, t.ck) + cdiv(c1, t.ck) == 1;
     const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
-    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d>", N == 32 ? 1 : 2, t.rt, t.ck,
-             stats ? "true" : "false", wconst ? "true" : "false", t.it);
+    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck,
+             stats ? "true" : "false", wconst ? "true" : "false", t.it, bns ? "true" : "false");
     return buf;
 }
 
 // wconst (one chunk per item): the weights are staged once per block. CK = 8 always has one chunk; CK = 16
 // (experiments) always takes the general instance, which is also correct with one chunk.
 template <int NT, int RT, int CK, int IT = 1>
-static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p) {
+static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p, bool bns = false) {
     constexpr bool W0 = CK == 8, W1 = CK != 16;  // the instance for wconst false / true
+    // BN-backward sums (dgrad STORE launches, sd_conv_gemm_bnsum); not NT 2 x RT 3 (the second accumulator set
+    // and the prefetched y pieces spill there: sd_halo_bnsum_ok)
+    if constexpr (CK == 32 && IT == 1 && !(NT == 2 && RT == 3)) {
+        if (bns) {
+            if (wconst ? W1 : W0)
+                hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1, IT, true>), grid, dim3(512), 0, st, p);
+            else
+                hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0, IT, true>), grid, dim3(512), 0, st, p);
+            return;
+        }
+    }
     if (stats && (wconst ? W1 : W0))
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W1, IT>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W1, IT, false>), grid, dim3(512), 0, st, p);
     else if (stats)
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W0, IT>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, true, W0, IT, false>), grid, dim3(512), 0, st, p);
     else if (wconst ? W1 : W0)
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1, IT>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1, IT, false>), grid, dim3(512), 0, st, p);
     else
-        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0, IT>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0, IT, false>), grid, dim3(512), 0, st, p);
 }
 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
-                     void* out1, int n_split, float* stats, hipStream_t st) {
+                     void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns) {
     const bool st_ = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_);
     HFwdArgs p;
@@ -1612,6 +1697,17 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.out1 = (__bf16*)out1;
     p.n_split = n_split;
     p.stats = stats;
+    p.by = nullptr;
+    p.bsc = p.bsh = p.bmu = p.bis = nullptr;
+    if (bns) {
+        SD_REQUIRE(epi == SD_EPI_STORE && t.ck == 32 && t.it == 1 && stats,
+                   "sd_conv_gemm_bnsum: STORE epilogue of a CK = 32 halo shape with a partials buffer");
+        p.by = (const __bf16*)bns->y;
+        p.bsc = bns->scale;
+        p.bsh = bns->shift;
+        p.bmu = bns->mean;
+        p.bis = bns->invstd;
+    }
     p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
     p.dbg = g_wg_dbg;
     SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= (t.it == 2 ? 384 : halo_px_cap(t.rt, t.ck)) && t.th * t.tw <= 128 * t.rt &&
@@ -1630,12 +1726,12 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
         else if (t.rt == 3) launch_halo<1, 3, 8>(st_, wc, grid, st, p);
         else launch_halo<1, 2, 8>(st_, wc, grid, st, p);
     } else if (N == 32) {
-        if (t.rt == 4) launch_halo<1, 4, 32>(st_, wc, grid, st, p);
-        else if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p);
-        else launch_halo<1, 2, 32>(st_, wc, grid, st, p);
+        if (t.rt == 4) launch_halo<1, 4, 32>(st_, wc, grid, st, p, bns);
+        else if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p, bns);
+        else launch_halo<1, 2, 32>(st_, wc, grid, st, p, bns);
     } else if (t.ck == 32) {
-        if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p);
-        else launch_halo<2, 2, 32>(st_, wc, grid, st, p);
+        if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p, bns);
+        else launch_halo<2, 2, 32>(st_, wc, grid, st, p, bns);
     } else if (t.it == 2) {  // RT = 2 only (RT = 3 with two accumulator sets spills)
         launch_halo<2, 2, 16, 2>(st_, wc, grid, st, p);
     } else if (t.rt == 4) {

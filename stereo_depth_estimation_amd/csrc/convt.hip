@@ -170,8 +170,12 @@ __global__ __launch_bounds__(256, 2) void k_convt_fwd(const CtArgs p) {
 // K <= 256, N = 4*C with C % 32 == 0 and N % 128 == 0 (up1..up3; up4's K = 512 weight slice would
 // hold one block per CU, and the tiled GEMM measured faster there: 79 vs 115 us at B=64)
 bool sd_convt_fwd_ok(const sd_src& a, int N, int epi) {
+    static const int kmax = [] {  // SD_CONVT_KMAX: largest K for k_convt_fwd (A/B runs)
+        const char* e = getenv("SD_CONVT_KMAX");
+        return e && atoi(e) > 0 ? atoi(e) : 256;
+    }();
     const int K = a.chans[0] + a.chans[1];
-    return epi == SD_EPI_PIXSHUF && a.taps == 1 && !a.pool && a.chans[1] == 0 && K % CT_KC == 0 && K <= 256 &&
+    return epi == SD_EPI_PIXSHUF && a.taps == 1 && !a.pool && a.chans[1] == 0 && K % CT_KC == 0 && K <= kmax &&
            N % CT_NB == 0 && (N / 4) % 32 == 0 && (a.xform[0] == SD_IDENT || a.xform[0] == SD_BNRELU);
 }
 

@@ -156,6 +156,10 @@ class UNetEngine:
         self.bn_fuse = os.environ.get("SD_BN_FUSE", "1") != "0"
         # bf16 training: ConvTranspose2d bias gradients from the decoder dgrad epilogue (SD_BIAS_FUSE=0: own pass)
         self.bias_fuse = os.environ.get("SD_BIAS_FUSE", "1") != "0"
+        # bf16 training: the BatchNorm-backward sums of a block's conv0 from its conv1 dgrad epilogue
+        # (sd_conv_gemm_bnsum; SD_BNSUM_FUSE=0: sd_bn_bwd_reduce pass)
+        self.bnsum_fuse = os.environ.get("SD_BNSUM_FUSE", "1") != "0"
+        self._bnsum_rows: dict[str, int] = {}
         self.params: dict[str, torch.Tensor] = {}
         self.grads: dict[str, torch.Tensor] = {}
         self.bufs: dict[str, torch.Tensor] = {}
@@ -582,8 +586,20 @@ class UNetEngine:
             dsrc = L.make_src(dy, cl.cout, Hl, Wl, taps=9)
             if cl.idx == 1:
                 out = t["da:" + cl.blk + ".0"]
-                L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d, L.SD_EPI_STORE,
-                       out.data_ptr(), None, 0, None, None, s)
+                c0 = self.convs[cl.blk + ".0"]
+                if (self.bnsum_fuse and dt == L.SD_BF16 and cl.cin <= 64
+                        and L.call("sd_conv_gemm_bnsum_ok", dt, dsrc, cl.cin) == 1):
+                    # da of conv0 and its BatchNorm-backward sums (for _bn_bwd(conv0)) from one launch. At 32/64
+                    # channels (240x320, 120x160) the epilogue's sums cost less than the reduce pass they replace;
+                    # deeper, the two measured equal (the epilogue is MFMA-wave time, the pass was HBM time)
+                    L.call("sd_conv_gemm_bnsum", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d,
+                           out.data_ptr(), t["y:" + c0.name].data_ptr(), t["scale:" + c0.name].data_ptr(),
+                           t["shift:" + c0.name].data_ptr(), t["mean:" + c0.name].data_ptr(),
+                           t["invstd:" + c0.name].data_ptr(), t["chan"].data_ptr(), s)
+                    self._bnsum_rows[c0.name] = L.call("sd_conv_gemm_bnsum_rows", dsrc, ws.B, Hl, Wl, cl.cin)
+                else:
+                    L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d,
+                           L.SD_EPI_STORE, out.data_ptr(), None, 0, None, None, s)
             elif cl.blk in PREV_ENC:
                 out = t["dpool:" + cl.blk]
                 L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d, L.SD_EPI_STORE,
@@ -646,7 +662,8 @@ class UNetEngine:
                 # dec1.1: heads() left its BN-backward sums in t["chan"]
                 fused_rows = getattr(self, "_heads_bn_rows", 0) if blk == "dec1" else 0
                 self._conv_bwd(self.convs[blk + ".1"], need_dgrad=True, fused_rows=fused_rows)
-            self._conv_bwd(self.convs[blk + ".0"], need_dgrad=(blk != "enc1"))
+            self._conv_bwd(self.convs[blk + ".0"], need_dgrad=(blk != "enc1"),
+                           fused_rows=self._bnsum_rows.pop(blk + ".0", 0))
             if grad_hook is not None:
                 grad_hook(blk)
             if blk in UP_OF_DEC:

@@ -541,3 +541,37 @@ def test_convT_fwd_identity_source():
     lib.call("sd_conv_gemm", lib.SD_BF16, src, B, h, w_, wpf.data_ptr(), 4 * co, 64, lib.SD_EPI_PIXSHUF,
              out.data_ptr(), None, 0, bd.data_ptr(), None, s)
     assert float((_from_nhwc(out, B, 2 * h, 2 * w_, co) - ref).abs().max()) <= _tol(ref, "bf16")
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 32, 64, 32, 32), (1, 48, 64, 32, 32), (2, 30, 40, 64, 64),
+                                         (1, 16, 64, 128, 64), (2, 24, 32, 64, 128), (1, 26, 50, 32, 64)])
+def test_conv_gemm_bnsum_matches_store_plus_reduce(B, H, W, ci, co):
+    """sd_conv_gemm_bnsum: the dgrad-style conv stores exactly what sd_conv_gemm(STORE) stores, and its partial rows
+    sum to sd_bn_bwd_reduce's BatchNorm-backward sums over (out, y)."""
+    lib = L()
+    torch.manual_seed(8)
+    s = lib.stream_handle()
+    x = torch.randn(B, ci, H, W)
+    w = torch.randn(co, ci, 3, 3) / (3 * ci ** 0.5)
+    wp, kpad = _pack3(w, ci, False, "bf16")
+    src = lib.make_src(_nhwc(x, "bf16"), ci, H, W, taps=9)
+    assert lib.call("sd_conv_gemm_bnsum_ok", lib.SD_BF16, src, co) == 1
+    y = (torch.randn(B * H * W, co) * 2 + 0.3).to(DEV, torch.bfloat16)
+    sc = ((torch.rand(co) + 0.5) * torch.where(torch.rand(co) < 0.2, -1.0, 1.0)).to(DEV)
+    sh, mean, invstd = (torch.randn(co) * 0.3).to(DEV), (torch.randn(co) * 0.2).to(DEV), (torch.rand(co) + 0.5).to(DEV)
+    out_ref = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=DEV)
+    lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, lib.SD_EPI_STORE, out_ref.data_ptr(),
+             None, 0, None, None, s)
+    rows_r = lib.call("sd_chan_reduce_rows", B * H * W, co)
+    part_r = torch.empty(rows_r, co, 2, device=DEV)
+    lib.call("sd_bn_bwd_reduce", lib.SD_BF16, out_ref.data_ptr(), y.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+             mean.data_ptr(), invstd.data_ptr(), B * H * W, co, part_r.data_ptr(), s)
+    out = torch.empty_like(out_ref)
+    rows = lib.call("sd_conv_gemm_bnsum_rows", src, B, H, W, co)
+    part = torch.full((rows, co, 2), float("nan"), device=DEV)
+    lib.call("sd_conv_gemm_bnsum", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, out.data_ptr(), y.data_ptr(),
+             sc.data_ptr(), sh.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(), s)
+    assert torch.equal(out, out_ref)
+    got, ref = part.double().sum(0).cpu(), part_r.double().sum(0).cpu()
+    scale = 1e-4 * (B * H * W) ** 0.5 * (1 + float(ref.abs().max()))
+    assert torch.allclose(got, ref, rtol=1e-4, atol=scale)
