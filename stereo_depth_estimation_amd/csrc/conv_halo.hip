@@ -272,7 +272,11 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = (my_items + IT - 1) / IT * nchunks;  // chunk iterations (block-uniform), IT items each
-    constexpr int LS = NT == 1 && CK == 8 ? 4 : 2;   // loader register sets (chunks in flight)
+#ifndef HC_LS_N32
+#define HC_LS_N32 2
+#endif
+    // loader register sets (chunks in flight); HC_LS_N32: for the 32-channel-chunk N = 32 instances (A/B builds)
+    constexpr int LS = NT == 1 && CK == 8 ? 4 : (NT == 1 && CK == 32 ? HC_LS_N32 : 2);
     const int padded = (total + LS - 1) / LS * LS;   // loader iterations
 
     // the BN affine of every input channel (identity for raw sources), read by the loaders per chunk from LDS
