@@ -282,15 +282,21 @@ int sd_halo_store_rows(int batch, int H, int W, int N, int ctot);
 bool sd_halo_bnsum_ok(const sd_src& a, int N);
 
 bool sd_convt_fwd_ok(const sd_src& a, int N, int epi);
-const char* sd_convt_fwd_name(const sd_src& a);
+const char* sd_convt_fwd_name(const sd_src& a, int N);
 int sd_convt_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, const float* bias,
                  void* out, hipStream_t st);
+bool sd_convt_dgrad_ok(const sd_src& a, int N, int epi);
+const char* sd_convt_dgrad_name(const sd_src& a, int N, bool bns);
+int sd_convt_dgrad_rows(const sd_src& a, int batch, int H, int W, int N);
+int sd_convt_dgrad(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, void* out,
+                   const HaloBnSum* bns, float* partials, hipStream_t st);
 
 extern "C" const char* sd_conv_gemm_kernel_name(int dtype, const sd_src* a, int batch, int H, int W, int N, int epi) {
     static thread_local char buf[96];
     const long long M = (long long)batch * H * W;
     if (dtype == SD_BF16 && a && sd_halo_fwd_ok(*a, N, epi)) return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1]);
-    if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, N, epi)) return sd_convt_fwd_name(*a);
+    if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, N, epi)) return sd_convt_fwd_name(*a, N);
+    if (dtype == SD_BF16 && a && sd_convt_dgrad_ok(*a, N, epi)) return sd_convt_dgrad_name(*a, N, false);
     if (dtype == SD_BF16 && a && !a->pool) return sd_fast_fwd_name(M, N);
     const Cfg c = pick_cfg(M, N);
     const int wm = c.bn == 32 ? 4 : 2, wn = c.bn == 32 ? 1 : 2;
@@ -344,6 +350,8 @@ extern "C" int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W,
         return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, epi, out0, out1, n_split, stats, to_stream(s));
     if (dtype == SD_BF16 && sd_convt_fwd_ok(*a, N, epi))
         return sd_convt_fwd(*a, batch, H, W, wpack, N, kpad, bias, out0, to_stream(s));
+    if (dtype == SD_BF16 && sd_convt_dgrad_ok(*a, N, epi))
+        return sd_convt_dgrad(*a, batch, H, W, wpack, N, kpad, out0, nullptr, nullptr, to_stream(s));
     if (dtype == SD_BF16 && !a->pool)
         return sd_fast_conv_gemm(*a, batch, H, W, wpack, N, kpad, epi, out0, out1, n_split, bias, stats, to_stream(s));
     // bf16 with an in-gather max pool: generic kernel (its stat-row count differs from the bf16 query)
@@ -359,15 +367,22 @@ extern "C" int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W,
     return launch_igemm(p, to_stream(s));
 }
 
+// the ConvTranspose2d dgrad (4-tap sub-pixel source) through k_convt, where sd_convt_dgrad_ok routes it
+static bool convt_bnsum_ok(const sd_src& a, int N) { return a.taps == 4 && sd_convt_dgrad_ok(a, N, SD_EPI_STORE); }
+
 extern "C" int sd_conv_gemm_bnsum_ok(int dtype, const sd_src* a, int N) {
-    return dtype == SD_BF16 && a && a->xform[0] != SD_AFFINE && a->xform[1] != SD_AFFINE && sd_halo_bnsum_ok(*a, N) ? 1 : 0;
+    if (dtype != SD_BF16 || !a || a->xform[0] == SD_AFFINE || a->xform[1] == SD_AFFINE) return 0;
+    return sd_halo_bnsum_ok(*a, N) || convt_bnsum_ok(*a, N) ? 1 : 0;
 }
 
 extern "C" int sd_conv_gemm_bnsum_rows(const sd_src* a, int batch, int H, int W, int N) {
-    return a ? sd_halo_store_rows(batch, H, W, N, a->chans[0] + a->chans[1]) : 0;
+    if (!a) return 0;
+    if (convt_bnsum_ok(*a, N)) return sd_convt_dgrad_rows(*a, batch, H, W, N);
+    return sd_halo_store_rows(batch, H, W, N, a->chans[0] + a->chans[1]);
 }
 
 extern "C" const char* sd_conv_gemm_bnsum_kernel_name(const sd_src* a, int H, int W, int N) {
+    if (a && convt_bnsum_ok(*a, N)) return sd_convt_dgrad_name(*a, N, true);
     if (!a || !sd_halo_bnsum_ok(*a, N)) return "";
     return sd_halo_fwd_name(H, W, N, SD_EPI_STORE, a->chans[0], a->chans[1], true);
 }
@@ -380,8 +395,13 @@ extern "C" int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, 
     SD_REQUIRE(batch > 0 && H > 0 && W > 0 && wpack && out && y && scale && shift && mean && invstd && partials,
                "sd_conv_gemm_bnsum: bad args");
     GatherSrc g = make_gather(*a);
-    SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == H && g.Wl == W, "sd_conv_gemm_bnsum: kpad/grid");
     const HaloBnSum bns{y, scale, shift, mean, invstd};
+    if (convt_bnsum_ok(*a, N)) {
+        SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == 2 * H && g.Wl == 2 * W,
+                   "sd_conv_gemm_bnsum: kpad/grid");
+        return sd_convt_dgrad(*a, batch, H, W, wpack, N, kpad, out, &bns, partials, to_stream(s));
+    }
+    SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == H && g.Wl == W, "sd_conv_gemm_bnsum: kpad/grid");
     return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, SD_EPI_STORE, out, nullptr, 0, partials, to_stream(s),
                             &bns);
 }

@@ -293,6 +293,11 @@ class UNetEngine:
                 max_chan = max(max_chan, L.call("sd_chan_reduce_rows", P, u.cout) * u.cout * 2)
                 sp = L.call("sd_wgrad_splits", dt, B, H >> lv, W >> lv, u.cin, 4 * u.cout)
                 max_slab = max(max_slab, sp * u.cin * 4 * u.cout)
+                # BatchNorm-backward rows of the ConvTranspose dgrad (sd_conv_gemm_bnsum)
+                dsrc = L.make_src(t["du:" + u.name], u.cout, H >> (lv - 1), W >> (lv - 1), taps=4)
+                if L.call("sd_conv_gemm_bnsum_ok", dt, dsrc, u.cin) == 1:
+                    rows = L.call("sd_conv_gemm_bnsum_rows", dsrc, B, H >> lv, W >> lv, u.cin)
+                    max_chan = max(max_chan, rows * u.cin * 2)
             for blk in ("enc2", "enc3", "enc4", "bottleneck"):
                 prev = self.convs[PREV_ENC[blk] + ".1"]
                 t["dpool:" + blk] = act(prev.level + 1, prev.cout)
@@ -633,8 +638,17 @@ class UNetEngine:
         a = L.make_src(t["y:" + src_cl.name], src_cl.cout, Hl, Wl, taps=1, bn0=self._bn(src_cl))
         b = L.make_src(du, u.cout, Hh, Wh, taps=4)
         self._wgrad(a, b, u.level, u.cin, 4 * u.cout, L.SD_W_CONVT, u.cin, self.grads[u.name + ".weight"])
-        L.call("sd_conv_gemm", dt, b, ws.B, Hl, Wl, self._wp(u.off_d), u.cin, u.kpad_d, L.SD_EPI_STORE,
-               t["da:" + src_cl.name].data_ptr(), None, 0, None, None, s)
+        if self.bnsum_fuse and L.call("sd_conv_gemm_bnsum_ok", dt, b, u.cin) == 1:
+            # da of the source conv and its BatchNorm-backward sums (for _bn_bwd(src_cl)) from one launch:
+            # the reduce pass over (da, y) that followed every ConvTranspose dgrad is gone
+            L.call("sd_conv_gemm_bnsum", dt, b, ws.B, Hl, Wl, self._wp(u.off_d), u.cin, u.kpad_d,
+                   t["da:" + src_cl.name].data_ptr(), t["y:" + src_cl.name].data_ptr(),
+                   t["scale:" + src_cl.name].data_ptr(), t["shift:" + src_cl.name].data_ptr(),
+                   t["mean:" + src_cl.name].data_ptr(), t["invstd:" + src_cl.name].data_ptr(), t["chan"].data_ptr(), s)
+            self._bnsum_rows[src_cl.name] = L.call("sd_conv_gemm_bnsum_rows", b, ws.B, Hl, Wl, u.cin)
+        else:
+            L.call("sd_conv_gemm", dt, b, ws.B, Hl, Wl, self._wp(u.off_d), u.cin, u.kpad_d, L.SD_EPI_STORE,
+                   t["da:" + src_cl.name].data_ptr(), None, 0, None, None, s)
 
     def backward(self, grad_hook=None):
         """Full backward after heads() wrote da:dec1.1 (model.py:79-104 in reverse).
@@ -659,8 +673,9 @@ class UNetEngine:
                        t["chan"].data_ptr() if fused else None, s)
                 self._conv_bwd(cl, need_dgrad=True, fused_rows=fused_rows)
             else:
-                # dec1.1: heads() left its BN-backward sums in t["chan"]
-                fused_rows = getattr(self, "_heads_bn_rows", 0) if blk == "dec1" else 0
+                # dec1.1: heads() left its BN-backward sums in t["chan"]; deeper layers: the ConvTranspose dgrad
+                # that wrote their da may have (sd_conv_gemm_bnsum in _up_bwd)
+                fused_rows = getattr(self, "_heads_bn_rows", 0) if blk == "dec1" else self._bnsum_rows.pop(blk + ".1", 0)
                 self._conv_bwd(self.convs[blk + ".1"], need_dgrad=True, fused_rows=fused_rows)
             self._conv_bwd(self.convs[blk + ".0"], need_dgrad=(blk != "enc1"),
                            fused_rows=self._bnsum_rows.pop(blk + ".0", 0))

@@ -535,7 +535,7 @@ def test_convT_fwd_identity_source():
     lib.call("sd_pack_convT_w", lib.SD_BF16, wt.contiguous().to(DEV).data_ptr(), ci, co, 0, 64, wpf.data_ptr(), s)
     src = lib.make_src(_nhwc(x, "bf16"), ci, h, w_, taps=1)
     assert lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, h, w_, 4 * co,
-                           lib.SD_EPI_PIXSHUF) == "k_convt_fwd<false>"
+                           lib.SD_EPI_PIXSHUF).startswith("k_convt<0, ")  # CT_FWD: no BN transform
     out = torch.empty(B * 4 * h * w_, co, dtype=torch.bfloat16, device=DEV)
     bd = bias.to(DEV)
     lib.call("sd_conv_gemm", lib.SD_BF16, src, B, h, w_, wpf.data_ptr(), 4 * co, 64, lib.SD_EPI_PIXSHUF,
@@ -574,4 +574,48 @@ def test_conv_gemm_bnsum_matches_store_plus_reduce(B, H, W, ci, co):
     assert torch.equal(out, out_ref)
     got, ref = part.double().sum(0).cpu(), part_r.double().sum(0).cpu()
     scale = 1e-4 * (B * H * W) ** 0.5 * (1 + float(ref.abs().max()))
+    assert torch.allclose(got, ref, rtol=1e-4, atol=scale)
+
+
+@pytest.mark.parametrize("B,h,w_,ci,co", [(2, 12, 20, 64, 32), (1, 15, 20, 128, 64), (3, 17, 23, 64, 32),
+                                          (2, 30, 40, 128, 64), (4, 60, 80, 64, 32)])
+def test_convT_dgrad_bnsum_matches_store_plus_reduce(B, h, w_, ci, co):
+    """ConvTranspose2d dgrad through k_convt (sub-pixel gather, weights resident in LDS): sd_conv_gemm_bnsum stores
+    exactly what sd_conv_gemm(STORE) stores, that matches F.conv_transpose2d's input gradient, and its partial rows sum
+    to sd_bn_bwd_reduce's BatchNorm-backward sums over (dx, y) (the BatchNorm of the conv feeding the ConvTranspose)."""
+    lib = L()
+    torch.manual_seed(9)
+    s = lib.stream_handle()
+    wt = (torch.randn(ci, co, 2, 2) / 8).to(torch.bfloat16).float().requires_grad_(True)
+    x = torch.randn(B, ci, h, w_).requires_grad_(True)
+    dout = torch.randn(B, co, 2 * h, 2 * w_).to(torch.bfloat16).float()
+    F.conv_transpose2d(x, wt, None, stride=2).backward(dout)
+    kd = ((4 * co + 63) // 64) * 64
+    wpd = torch.empty(ci * kd, dtype=torch.bfloat16, device=DEV)
+    lib.call("sd_pack_convT_w", lib.SD_BF16, wt.detach().contiguous().to(DEV).data_ptr(), ci, co, 1, kd, wpd.data_ptr(), s)
+    dsrc = lib.make_src(_nhwc(dout, "bf16"), co, 2 * h, 2 * w_, taps=4)
+    assert lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, dsrc, B, h, w_, ci,
+                           lib.SD_EPI_STORE).startswith("k_convt<2, ")
+    assert lib.call("sd_conv_gemm_bnsum_ok", lib.SD_BF16, dsrc, ci) == 1
+    P = B * h * w_
+    out_ref = torch.empty(P, ci, dtype=torch.bfloat16, device=DEV)
+    lib.call("sd_conv_gemm", lib.SD_BF16, dsrc, B, h, w_, wpd.data_ptr(), ci, kd, lib.SD_EPI_STORE, out_ref.data_ptr(),
+             None, 0, None, None, s)
+    assert float((_from_nhwc(out_ref, B, h, w_, ci) - x.grad).abs().max()) <= _tol(x.grad, "bf16")
+    y = (torch.randn(P, ci) * 2 + 0.3).to(DEV, torch.bfloat16)
+    sc = ((torch.rand(ci) + 0.5) * torch.where(torch.rand(ci) < 0.2, -1.0, 1.0)).to(DEV)
+    sh, mean, invstd = (torch.randn(ci) * 0.3).to(DEV), (torch.randn(ci) * 0.2).to(DEV), (torch.rand(ci) + 0.5).to(DEV)
+    rows_r = lib.call("sd_chan_reduce_rows", P, ci)
+    part_r = torch.empty(rows_r, ci, 2, device=DEV)
+    lib.call("sd_bn_bwd_reduce", lib.SD_BF16, out_ref.data_ptr(), y.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+             mean.data_ptr(), invstd.data_ptr(), P, ci, part_r.data_ptr(), s)
+    out = torch.empty_like(out_ref)
+    rows = lib.call("sd_conv_gemm_bnsum_rows", dsrc, B, h, w_, ci)
+    part = torch.full((rows, ci, 2), float("nan"), device=DEV)
+    lib.call("sd_conv_gemm_bnsum", lib.SD_BF16, dsrc, B, h, w_, wpd.data_ptr(), ci, kd, out.data_ptr(), y.data_ptr(),
+             sc.data_ptr(), sh.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(), s)
+    assert lib.kernel_name("sd_conv_gemm_bnsum_kernel_name", dsrc, h, w_, ci).startswith("k_convt<3, ")
+    assert torch.equal(out, out_ref)
+    got, ref = part.double().sum(0).cpu(), part_r.double().sum(0).cpu()
+    scale = 1e-4 * P ** 0.5 * (1 + float(ref.abs().max()))
     assert torch.allclose(got, ref, rtol=1e-4, atol=scale)
