@@ -49,18 +49,21 @@ __device__ __forceinline__ Affine8 load_affine(bool bn, const float* sc, const f
     a.h1 = *reinterpret_cast<const float4*>(h + 4);
     return a;
 }
+// relu(scale*x + shift) of 8 bf16 values: the ReLU is taken on the rounded bf16 pair (v_pk_max_i16 against 0: a
+// bf16 is <= 0 exactly when its sign bit is set or it is zero, and rounding preserves the sign), one conversion
+// and one max per pair (the per-element form took ~4.5 VALU per element in loaders that are VALU-bound)
 __device__ __forceinline__ uint4 xform_reg(uint4 raw, const Affine8& a) {
     const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
     const float s[8] = {a.s0.x, a.s0.y, a.s0.z, a.s0.w, a.s1.x, a.s1.y, a.s1.z, a.s1.w};
     const float h[8] = {a.h0.x, a.h0.y, a.h0.z, a.h0.w, a.h1.x, a.h1.y, a.h1.z, a.h1.w};
-    bf16x8 b;
+    unsigned o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
-        b[2 * i] = (__bf16)fmaxf(__builtin_fmaf(lo, s[2 * i], h[2 * i]), 0.f);
-        b[2 * i + 1] = (__bf16)fmaxf(__builtin_fmaf(hi, s[2 * i + 1], h[2 * i + 1]), 0.f);
+        const float lo = __builtin_fmaf(__uint_as_float(w[i] << 16), s[2 * i], h[2 * i]);
+        const float hi = __builtin_fmaf(__uint_as_float(w[i] & 0xffff0000u), s[2 * i + 1], h[2 * i + 1]);
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2\n\tv_pk_max_i16 %0, %0, 0" : "=v"(o[i]) : "v"(lo), "v"(hi));
     }
-    return *reinterpret_cast<uint4*>(&b);
+    return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 struct SrcF {  // unpooled gather source, bf16
@@ -170,7 +173,10 @@ struct FwdArgs {
     float* stats;
 };
 
-template <int BM, int BN, int WM, int WN>
+// FA: one unpooled source tensor with 1 tap (on the grid) or 4 sub-pixel taps (at twice its resolution), K a whole
+// number of 64-wide tiles, 32-bit offsets: each row's base offset is computed once and a K tile adds the tap's
+// constant offset (the general gather's per-load tap test and 64-bit address math paced the ConvTranspose GEMMs)
+template <int BM, int BN, int WM, int WN, bool FA>
 __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
     constexpr int WTM = BM / WM, WTN = BN / WN, RM = WTM / 16, RN = WTN / 16;
     constexpr int AR = BM / 32, BR = (BN + 31) / 32;  // rows per thread (8 chunks per row, 32 rows per pass)
@@ -198,6 +204,13 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
     }
     KCursor kc;
     kc.init(j, p.a.cpt);
+    // FA: the row's source pixel for tap 0 (taps 4: (2h, 2w) at 2x resolution)
+    uint32_t pbase[AR];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+        const uint32_t r = (uint32_t)rb[i] * p.H + rh[i];
+        pbase[i] = p.a.taps == 4 ? 4 * r * p.W + 2 * rw[i] : r * p.W + rw[i];
+    }
 
     f32x4 acc[RM][RN];
 #pragma unroll
@@ -213,6 +226,18 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
 
     auto load_tile = [&](int kt) {
         const int tap = kc.tap;
+        if constexpr (FA) {
+            const int c = kc.cc * 8;
+            acs.xf = p.a.x0;
+            aff = load_affine(acs.xf == SD_BNRELU, p.a.sc0 + c, p.a.sh0 + c, p.wp);
+            const uint32_t toff = p.a.taps == 4 ? (uint32_t)((tap >> 1) * 2 * p.W + (tap & 1)) : 0u;
+#pragma unroll
+            for (int i = 0; i < AR; ++i) {
+                ain[i] = rv[i];
+                const uint32_t off = rv[i] ? (pbase[i] + toff) * (uint32_t)p.a.c0 + c : 0u;
+                ra[i] = *reinterpret_cast<const uint4*>(p.a.p0 + off);
+            }
+        } else {
         acs = select_chunk(p.a, kc.cc);
         aff = load_affine(acs.xf == SD_BNRELU, acs.sc, acs.sh, p.wp);
 #pragma unroll
@@ -220,6 +245,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
             int hs = 0, ws = 0;
             ain[i] = rv[i] & tap_pixel(p.a, tap, rh[i], rw[i], hs, ws);
             ra[i] = load_px(p.a, acs, ain[i], rb[i], hs, ws);
+        }
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
@@ -384,7 +410,11 @@ __device__ __forceinline__ bf16x8 frag_tr64(const __bf16* lds, int ld, int col0,
     return r;
 }
 
-template <int BM, int BN, int WM, int WN>
+// CT: the ConvTranspose2d weight gradient (A = a 1x1 source on the GEMM grid, B = the 4-tap sub-pixel source at
+// twice its resolution). Pixel m = r*W + w of the grid reads A at m*Ca and B at (4*r*W + 2*w + toff)*Cb with 32-bit
+// element offsets: one division per B load instead of two per load plus the general tap test (the loader's VALU,
+// ~240 per 64-pixel tile per lane in the general form, paced these layers at ~300 TFLOP/s)
+template <int BM, int BN, int WM, int WN, bool CT>
 __global__ __launch_bounds__(256) void k_wgrad_bf16(const WgfArgs p) {
     constexpr int BKP = 64;
     constexpr int LDA = BM + 16, LDB = BN + 16;
@@ -424,9 +454,31 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(const WgfArgs p) {
 
     uint4 ra[AL], rbv[BL];
     bool av[AL], bv_[BL];
+    // CT: B's tap offset in sub-pixels, and the sources' element bases of this thread's fixed chunk columns
+    const uint32_t btoff = (uint32_t)((b_tap >> 1) * 2 * p.W + (b_tap & 1));
+    const __bf16* abase = acs.base + acs.c;
+    const __bf16* bbase = bcs.base + bcs.c;
     // branch-free gathers (see load_px): every lane issues its loads, invalid ones read a safe address
     auto load_tile = [&](int t) {
         const int pt = p_begin + t * BKP;
+        if constexpr (CT) {
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int px = pt + apr + i * APR;
+                av[i] = a_ok & (px < p_end);
+                const uint32_t m = av[i] ? px : 0;
+                ra[i] = *reinterpret_cast<const uint4*>(abase + m * (uint32_t)acs.C);
+            }
+#pragma unroll
+            for (int i = 0; i < BL; ++i) {
+                const int px = pt + bpr + i * BPR;
+                bv_[i] = b_ok & (px < p_end);
+                const uint32_t m = bv_[i] ? px : 0;
+                const uint32_t r = fdiv(m, p.fW), w = m - r * p.W;
+                rbv[i] = *reinterpret_cast<const uint4*>(bbase + ((4 * r * p.W + 2 * w + btoff) * (uint32_t)bcs.C));
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < AL; ++i) {
             const int px = pt + apr + i * APR;
@@ -559,20 +611,44 @@ FCfg pick_wg(int M, int N) {
 
 }  // namespace
 
+// SD_FFA=0: the general gather for the ConvTranspose-shaped implicit GEMMs too (A/B runs)
+static bool ffa_shape(const sd_src& a) {
+    static const bool on = [] {
+        const char* e = getenv("SD_FFA");
+        return !(e && atoi(e) == 0);
+    }();
+    return on && !a.pool && a.chans[1] == 0 && (a.taps == 1 || a.taps == 4) && (a.chans[0] * (a.taps == 4 ? 4 : 1)) % 64 == 0;
+}
+
 // ---------------------------------------------------------------------- host dispatch (bf16)
 int sd_fast_fwd_rows(long long M, int N) { return cdiv(M, pick_fwd(M, N).bm); }
 
-const char* sd_fast_fwd_name(long long M, int N) {
+const char* sd_fast_fwd_name(const sd_src& a, long long M, int N) {
     static thread_local char buf[96];
     const FCfg c = pick_fwd(M, N);
-    snprintf(buf, sizeof(buf), "k_conv_fwd_bf16<%d, %d, %d, %d>", c.bm, c.bn, c.wm, c.wn);
+    snprintf(buf, sizeof(buf), "k_conv_fwd_bf16<%d, %d, %d, %d, %s>", c.bm, c.bn, c.wm, c.wn, ffa_shape(a) ? "true" : "false");
     return buf;
 }
 
-const char* sd_fast_wgrad_name(int M, int N) {
+// SD_FWG_CT=0: the general gather for the ConvTranspose weight gradients too (A/B runs)
+static bool fwg_ct_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SD_FWG_CT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+static bool fwg_ct_shape(const sd_src& a, const sd_src& b) {
+    return a.taps == 1 && b.taps == 4 && !a.pool && !b.pool && a.chans[1] == 0 && b.chans[1] == 0 && b.H == 2 * a.H &&
+           b.W == 2 * a.W && fwg_ct_enabled();
+}
+
+const char* sd_fast_wgrad_name(const sd_src& a, const sd_src& b, int M, int N) {
     static thread_local char buf[96];
     const FCfg c = pick_wg(M, N);
-    snprintf(buf, sizeof(buf), "k_wgrad_bf16<%d, %d, %d, %d>", c.bm, c.bn, c.wm, c.wn);
+    snprintf(buf, sizeof(buf), "k_wgrad_bf16<%d, %d, %d, %d, %s>", c.bm, c.bn, c.wm, c.wn,
+             fwg_ct_shape(a, b) ? "true" : "false");
     return buf;
 }
 
@@ -612,14 +688,24 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
     p.stats = stats;
     const FCfg c = pick_fwd(M, N);
     dim3 grid(cdiv(M, c.bm), cdiv(N, c.bn));
-    if (c.bn == 32)
-        hipLaunchKernelGGL((k_conv_fwd_bf16<256, 32, 4, 1>), grid, dim3(256), 0, st, p);
+    const bool fa = ffa_shape(a) && p.a.kchunks % FKC == 0 && (long long)M * (a.taps == 4 ? 4 : 1) * a.chans[0] < (1LL << 31);
+    if (fa) {
+        if (c.bn == 32)
+            hipLaunchKernelGGL((k_conv_fwd_bf16<256, 32, 4, 1, true>), grid, dim3(256), 0, st, p);
+        else if (c.bn == 64)
+            hipLaunchKernelGGL((k_conv_fwd_bf16<128, 64, 2, 2, true>), grid, dim3(256), 0, st, p);
+        else if (c.bm == 128)
+            hipLaunchKernelGGL((k_conv_fwd_bf16<128, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
+        else
+            hipLaunchKernelGGL((k_conv_fwd_bf16<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
+    } else if (c.bn == 32)
+        hipLaunchKernelGGL((k_conv_fwd_bf16<256, 32, 4, 1, false>), grid, dim3(256), 0, st, p);
     else if (c.bn == 64)
-        hipLaunchKernelGGL((k_conv_fwd_bf16<128, 64, 2, 2>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((k_conv_fwd_bf16<128, 64, 2, 2, false>), grid, dim3(256), 0, st, p);
     else if (c.bm == 128)
-        hipLaunchKernelGGL((k_conv_fwd_bf16<128, 128, 2, 2>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((k_conv_fwd_bf16<128, 128, 2, 2, false>), grid, dim3(256), 0, st, p);
     else
-        hipLaunchKernelGGL((k_conv_fwd_bf16<64, 128, 2, 2>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((k_conv_fwd_bf16<64, 128, 2, 2, false>), grid, dim3(256), 0, st, p);
     return sd_check_launch("sd_conv_gemm(bf16 fast)");
 }
 
@@ -639,12 +725,22 @@ int sd_fast_wgrad_gemm(const sd_src& a, const sd_src& b, int batch, int H, int W
     p.slab = slab;
     const FCfg c = pick_wg(M, N);
     dim3 grid(cdiv(M, c.bm), cdiv(N, c.bn), splits);
-    if (c.bm == 32)
-        hipLaunchKernelGGL((k_wgrad_bf16<32, 128, 1, 4>), grid, dim3(256), 0, st, p);
+    // ConvTranspose2d shape: one 1x1 source without a pool, a 4-tap sub-pixel source of one tensor, 32-bit offsets
+    const bool ct = fwg_ct_shape(a, b) && a.H == H && a.W == W && (long long)p.P * a.chans[0] < (1LL << 31) &&
+                    4LL * p.P * b.chans[0] < (1LL << 31);
+    if (ct) {
+        if (c.bm == 32)
+            hipLaunchKernelGGL((k_wgrad_bf16<32, 128, 1, 4, true>), grid, dim3(256), 0, st, p);
+        else if (c.bm == 64)
+            hipLaunchKernelGGL((k_wgrad_bf16<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
+        else
+            hipLaunchKernelGGL((k_wgrad_bf16<128, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
+    } else if (c.bm == 32)
+        hipLaunchKernelGGL((k_wgrad_bf16<32, 128, 1, 4, false>), grid, dim3(256), 0, st, p);
     else if (c.bm == 64)
-        hipLaunchKernelGGL((k_wgrad_bf16<64, 128, 2, 2>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((k_wgrad_bf16<64, 128, 2, 2, false>), grid, dim3(256), 0, st, p);
     else
-        hipLaunchKernelGGL((k_wgrad_bf16<128, 128, 2, 2>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((k_wgrad_bf16<128, 128, 2, 2, false>), grid, dim3(256), 0, st, p);
     return sd_check_launch("sd_wgrad_gemm(bf16 fast)");
 }
 

@@ -189,24 +189,30 @@ __device__ __forceinline__ void wg_store(float* dw, long long e, float v, int N,
     }
 }
 
+// G split groups per block (8 or 32), 256 / G float4 outputs per block, 4 independent accumulators per lane: each
+// output quad sums its splits in a fixed order (deterministic for a given split count and G). Small layers have
+// few output quads and many splits (up to 512): G = 32 keeps 16 loads per output in flight instead of 4 (the
+// 8-group form was one dependent memory round trip per 32 splits, 9-12 us for layers of a few KB)
+template <int G>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ slab, int splits, int M, int N,
                                                       int layout, int ci_pad, int ci_real, float* __restrict__ dw) {
+    constexpr int QB = 256 / G;  // output quads per block
     const long long total = (long long)M * N;  // a multiple of 4 (N = 9*ci_pad or 4*co, ci_pad % 8 == 0)
     const long long total4 = total / 4;
-    __shared__ float4 part[8][32];
-    const int el = threadIdx.x & 31, g = threadIdx.x >> 5;
+    __shared__ float4 part[G][QB];
+    const int el = threadIdx.x % QB, g = threadIdx.x / QB;
     const float4* s4 = reinterpret_cast<const float4*>(slab);
-    for (long long q0 = (long long)blockIdx.x * 32; q0 < total4; q0 += (long long)gridDim.x * 32) {
+    for (long long q0 = (long long)blockIdx.x * QB; q0 < total4; q0 += (long long)gridDim.x * QB) {
         const long long q = q0 + el;
         float4 acc[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (q < total4) {
             int z = g;
-            for (; z + 24 < splits; z += 32) {
+            for (; z + 3 * G < splits; z += 4 * G) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const float4 v = s4[(size_t)(z + 8 * u) * total4 + q];
+                    const float4 v = s4[(size_t)(z + G * u) * total4 + q];
                     acc[u].x += v.x;
                     acc[u].y += v.y;
                     acc[u].z += v.z;
@@ -215,8 +221,8 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
             }
 #pragma unroll
             for (int u = 0; u < 3; ++u) {  // the < 4 remaining splits of this group
-                if (z + 8 * u < splits) {
-                    const float4 v = s4[(size_t)(z + 8 * u) * total4 + q];
+                if (z + G * u < splits) {
+                    const float4 v = s4[(size_t)(z + G * u) * total4 + q];
                     acc[u].x += v.x;
                     acc[u].y += v.y;
                     acc[u].z += v.z;
@@ -230,7 +236,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
         if (g == 0 && q < total4) {
             float4 t = part[0][el];
 #pragma unroll
-            for (int k = 1; k < 8; ++k) {
+            for (int k = 1; k < G; ++k) {
                 const float4 v = part[k][el];
                 t.x += v.x;
                 t.y += v.y;
@@ -251,7 +257,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
 
 int sd_validate_src(const sd_src* s, const char* what);
 // bf16 fast path (conv_fast.hip)
-const char* sd_fast_wgrad_name(int M, int N);
+const char* sd_fast_wgrad_name(const sd_src& a, const sd_src& b, int M, int N);
 int sd_fast_wgrad_splits(long long P, int M, int N);
 int sd_fast_wgrad_gemm(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab,
                        int splits, hipStream_t st);
@@ -268,7 +274,7 @@ extern "C" const char* sd_wgrad_kernel_name(int dtype, const sd_src* a, const sd
     static thread_local char buf[96];
     if (dtype == SD_BF16 && a && b && sd_halo_wgrad_ok(*a, *b, M))
         return sd_halo_wgrad_name(M, N, b->chans[0], a->H, a->W, false);
-    if (dtype == SD_BF16 && a && b && !a->pool && !b->pool) return sd_fast_wgrad_name(M, N);
+    if (dtype == SD_BF16 && a && b && !a->pool && !b->pool) return sd_fast_wgrad_name(*a, *b, M, N);
     const WCfg c = pick_wcfg(M, N);
     snprintf(buf, sizeof(buf), "k_wgemm<%s, %d, %d, 2, 2>", dtype == SD_BF16 ? "__bf16" : "float", c.bm, c.bn);
     return buf;
@@ -369,9 +375,20 @@ extern "C" int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int 
     SD_REQUIRE(layout != SD_W_CONV3 || ci_pad % 4 == 0, "sd_wgrad_reduce: ci_pad %d not a multiple of 4", ci_pad);
     SD_REQUIRE(((uintptr_t)slab & 15) == 0, "sd_wgrad_reduce: slab not 16-B aligned");
     const long long total4 = (long long)M * N / 4;
-    long long nb = (total4 + 31) / 32;
+    // 32 split groups where 8 would give less than two blocks per CU (SD_WGRED_G=8 forces the old form, A/B runs)
+    static const int g_env = [] {
+        const char* e = getenv("SD_WGRED_G");
+        return e ? atoi(e) : 0;
+    }();
+    const bool wide = g_env ? g_env == 32 : (total4 + 31) / 32 < 512 && splits >= 64;
+    const int qb = wide ? 8 : 32;
+    long long nb = (total4 + qb - 1) / qb;
     const int blocks = (int)(nb > 8192 ? 8192 : nb);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout, ci_pad,
-                       ci_real, dw);
+    if (wide)
+        hipLaunchKernelGGL(k_wgrad_reduce<32>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
+                           ci_pad, ci_real, dw);
+    else
+        hipLaunchKernelGGL(k_wgrad_reduce<8>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
+                           ci_pad, ci_real, dw);
     return sd_check_launch("sd_wgrad_reduce");
 }
