@@ -1231,11 +1231,12 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             }
             hgeo[i / 2] = e[0] | e[1] << 16;
         }
-        // the block's CIB x channels come from one source (the dispatcher requires chans[0] % CIB == 0)
-        const bool src1 = cc * CIB >= p.x.c0;
-        const __bf16* xsrc = src1 ? p.x.p1 : p.x.p0;
-        const int xC = src1 ? p.x.c1 : p.x.c0;
-        const HaloCol hc = halo_col(p.x, cc * CIB + xpiece * 8, p.slab);  // this thread's 8 channels (BN affine; slab: any valid address)
+        // this thread's 8 x channels (fixed piece): their source, channel stride and BN affine (slab: any valid
+        // address). Per thread, so a block's CIB channels may span both sources of a concatenation (dec1.0: 32 + 32
+        // in one 64-channel block, whose dy transform then runs once instead of once per 32-channel block)
+        const HaloCol hc = halo_col(p.x, cc * CIB + xpiece * 8, p.slab);
+        const __bf16* xsrc = hc.base;
+        const int xC = hc.C;
         // Per-piece element offsets from the tile origin (h0, w0), fixed for the launch: a piece's buffer
         // offset is then one add, its bounds test four compares against per-tile scalars, and a piece
         // outside the image / tile gets an offset past the buffer's range, which the buffer load returns
@@ -1789,7 +1790,12 @@ static WsCfg wgrad_ws(int M, int N, int c0 = -1) {
     const int ctot = N / 9;
     WsCfg c{M % 64 == 0 ? 64 : (M == 32 ? 32 : 0), 0};
     if (!on || c.cout == 0 || N % 9) return {0, 0};
-    if (ctot % 64 == 0 && (c0 < 0 || c0 % 64 == 0)) c.cib = 64;
+    // SD_WS_CIB64=0: 64-channel blocks only where the first source is a multiple of 64 (A/B runs)
+    static const bool span = [] {
+        const char* e = getenv("SD_WS_CIB64");
+        return !(e && atoi(e) == 0);
+    }();
+    if (ctot % 64 == 0 && (c0 < 0 || c0 % 64 == 0 || (span && c0 % 8 == 0))) c.cib = 64;
     else if (ctot % 32 == 0 && (c0 < 0 || c0 % 32 == 0)) c.cib = 32;
     return c.cib ? c : WsCfg{0, 0};
 }

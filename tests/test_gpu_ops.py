@@ -619,3 +619,46 @@ def test_convT_dgrad_bnsum_matches_store_plus_reduce(B, h, w_, ci, co):
     got, ref = part.double().sum(0).cpu(), part_r.double().sum(0).cpu()
     scale = 1e-4 * P ** 0.5 * (1 + float(ref.abs().max()))
     assert torch.allclose(got, ref, rtol=1e-4, atol=scale)
+
+
+@pytest.mark.parametrize("B,H,W,c0,c1,co", [(2, 24, 64, 32, 32, 32), (1, 20, 30, 32, 32, 64), (2, 16, 40, 32, 96, 32)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_conv3x3_wgrad_dual_source_spanning_block(B, H, W, c0, c1, co, fused):
+    """Weight gradient over cat([up, skip]) (model.py:89-95) where a 64-channel x block spans both sources (dec1.0:
+    32 + 32): each loader thread takes its 8 channels from its own source; plain and BatchNorm-backward-fused forms."""
+    lib = L()
+    torch.manual_seed(11)
+    ys = [torch.randn(B, c, H, W).to(torch.bfloat16).float() for c in (c0, c1)]
+    bns = [((torch.rand(c) + 0.5) * torch.where(torch.rand(c) < 0.2, -1.0, 1.0), torch.randn(c) * 0.3) for c in (c0, c1)]
+    x = torch.cat([torch.relu(y * s.view(1, -1, 1, 1) + h.view(1, -1, 1, 1)).to(torch.bfloat16).float()
+                   for y, (s, h) in zip(ys, bns)], 1)
+    ci = c0 + c1
+    dy = torch.randn(B, co, H, W).to(torch.bfloat16).float()
+    b = lib.make_src(_nhwc(ys[0], "bf16"), c0, H, W, taps=9, bn0=tuple(t.to(DEV) for t in bns[0]),
+                     src1=_nhwc(ys[1], "bf16"), c1=c1, bn1=tuple(t.to(DEV) for t in bns[1]))
+    sp = lib.call("sd_wgrad_splits", lib.SD_BF16, B, H, W, co, 9 * ci)
+    slab = torch.empty(sp * co * 9 * ci, device=DEV)
+    dw = torch.empty(co, ci, 3, 3, device=DEV)
+    s = lib.stream_handle()
+    if fused:  # dy from (da, y) with coef = (scale, 0, 0) and y > 0 everywhere: dy = scale * da
+        yo = (torch.rand(B, co, H, W) + 0.5).to(torch.bfloat16).float()
+        sc = torch.rand(co) + 0.5
+        dev = [t.to(DEV).contiguous() for t in (sc, torch.zeros(co), torch.zeros(co), torch.ones(co),
+                                                torch.stack([sc, torch.zeros(co), torch.zeros(co)], 1))]
+        dy = (sc.view(1, -1, 1, 1) * dy).to(torch.bfloat16).float()
+        dyd = torch.full((B * H * W, co), float("nan"), dtype=torch.bfloat16, device=DEV)
+        a = lib.make_src(dyd, co, H, W, taps=1)
+        assert lib.call("sd_wgrad_bnbwd_ok", lib.SD_BF16, a, b, co, 9 * ci) == ci // 64
+        dad, yod = _nhwc(dy / sc.view(1, -1, 1, 1), "bf16"), _nhwc(yo, "bf16")  # held: no buffer reuse mid-call
+        lib.call("sd_wgrad_gemm_bnbwd", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, dad.data_ptr(), yod.data_ptr(),
+                 *[t.data_ptr() for t in dev], slab.data_ptr(), sp, s)
+    else:
+        a = lib.make_src(_nhwc(dy, "bf16"), co, H, W, taps=1)
+        lib.call("sd_wgrad_gemm", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, slab.data_ptr(), sp, s)
+    lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(), s)
+    w = torch.zeros(co, ci, 3, 3, requires_grad=True)
+    F.conv2d(x, w, padding=1).backward(dy)
+    ref = w.grad
+    assert float((dw.cpu() - ref).abs().max()) <= 2e-2 * (1 + float(ref.abs().max()))
+    if fused:
+        assert not torch.isnan(_from_nhwc(dyd, B, H, W, co)).any()
