@@ -373,8 +373,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             else return st3;
         };
         uint4 wr[W_PER_THREAD];
-        // WCONST (one chunk per item): the weights are the same for every item of this block (fixed N-block),
-        // so they are loaded once and stored into both LDS buffers in the prologue
+        // WCONST (one or two chunks per item): the weights of chunk c are the same for every item of this block
+        // (fixed N-block), and with at most two chunks chunk c of every item lands in LDS buffer c (g & 1 == g % 2):
+        // they are loaded once and stored into the two buffers in the prologue (one chunk: into both). Two-chunk
+        // layers (64 input channels: enc2.1, dec2.1, enc3.0, dec1.0, ...) re-staged 36-72 KB of weights per item
         int w_cc = 0;  // chunk (within the item) of the next weights to load
         auto load_w = [&]() __attribute__((always_inline)) {  // weights of chunk w_cc -> wr, then advance
             const bool s1 = w_cc >= nc0;
@@ -503,8 +505,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             // sched barriers: the issue order must be an iteration's (the scheduler may swap independent sets)
             geometry();
             if constexpr (WCONST) {
-                load_w();
+                load_w();  // chunk 0
                 store_w(0);
+                load_w();  // chunk 1 (chunk 0 again with one chunk per item)
                 store_w(1);
             }
             load(S0);
@@ -1641,19 +1644,29 @@ bool sd_halo_bnsum_ok(const sd_src& a, int N) {
     return t.ck == 32 && t.it == 1 && !(N != 32 && t.rt == 3);
 }
 
+// weights resident in LDS for the whole launch (k_halo_conv WCONST): one or two chunks per item (SD_HALO_WC2=0: one
+// only, A/B runs)
+static bool wconst_chunks(int nchunks) {
+    static const bool two = [] {
+        const char* e = getenv("SD_HALO_WC2");
+        return !(e && atoi(e) == 0);
+    }();
+    return nchunks == 1 || (two && nchunks == 2);
+}
+
 // the instance as rocprofv3 names it: k_halo_conv<NT, RT, CK, STATS, WCONST> (launch_halo's choice)
 const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns) {
     static thread_local char buf[64];
     const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
-    const bool wc = cdiv(c0, t.ck) + cdiv(c1, t.ck) == 1;
+    const bool wc = wconst_chunks(cdiv(c0, t.ck) + cdiv(c1, t.ck));
     const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
     snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck,
              stats ? "true" : "false", wconst ? "true" : "false", t.it, bns ? "true" : "false");
     return buf;
 }
 
-// wconst (one chunk per item): the weights are staged once per block. CK = 8 always has one chunk; CK = 16
+// wconst (one or two chunks per item): the weights are staged once per block. CK = 8 always has one chunk; CK = 16
 // (experiments) always takes the general instance, which is also correct with one chunk.
 template <int NT, int RT, int CK, int IT = 1>
 static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p, bool bns = false) {
@@ -1724,8 +1737,9 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
                    (1LL << 31) && (long long)N * kpad * 2 < (1LL << 31) && (long long)H * W * N * 2 < (1LL << 31),
                "sd_conv_gemm(halo): image %dx%d or weights %dx%d too large for 32-bit offsets", H, W, N, kpad);
     const dim3 grid(p.gper * p.nblk);
-    const bool wc = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck) == 1;
-    SD_REQUIRE(t.ck != 8 || wc, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
+    const int nch = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck);
+    const bool wc = wconst_chunks(nch);
+    SD_REQUIRE(t.ck != 8 || nch == 1, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
     if (t.ck == 8) {
         if (t.rt == 4) launch_halo<1, 4, 8>(st_, wc, grid, st, p);
         else if (t.rt == 3) launch_halo<1, 3, 8>(st_, wc, grid, st, p);

@@ -112,7 +112,8 @@ class DataParallel:
                    count_hook=self._allreduce_count, before_step=ar.wait)
 
     def _allreduce_count(self, count: torch.Tensor):
-        dist.all_reduce(count, op=dist.ReduceOp.SUM, group=self.group)
+        """Async: train_step waits on the handle after the forward, so the collective's latency overlaps it."""
+        return dist.all_reduce(count, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def sum_metrics(self, t: torch.Tensor) -> torch.Tensor:
         t = t.clone()

@@ -47,17 +47,19 @@ def train_step(model: StereoUNet, optimizer: FusedAdamW | None, inputs, targets,
 
     Accumulates (sum nll, sum |d|, sum d^2, sum sigma, n) into ``model._engine.metrics``.
     grad_hook(name) is called as each top-level module's gradients become final (DDP buckets);
-    count_hook(count) may all-reduce the valid count before the loss normalisation.
+    count_hook(count) may all-reduce the valid count before the loss normalisation; if it returns a handle
+    (an async collective), the handle is waited on after the forward, which the collective then overlaps.
     """
     eng = model.engine(inputs.device)
     training = optimizer is not None
     mask_u8 = valid_mask.contiguous().view(torch.uint8)
     targets = targets.contiguous()
+    eng.count_valid(targets, mask_u8)  # depends on the batch only: counted (and all-reduced) ahead of the forward
+    pending = count_hook(eng.count) if count_hook is not None else None
     eng.pack_weights()
     eng.forward(inputs, train=training)
-    eng.count_valid(targets, mask_u8)
-    if count_hook is not None:
-        count_hook(eng.count)
+    if pending is not None:
+        pending.wait()
     if not training:
         eng.heads(L.SD_HEADS_LOSS, target=targets, valid=mask_u8, no_grad=True)
         return

@@ -291,3 +291,27 @@ def test_eval_forward_reuses_packs_and_tracks_weight_changes(precision):
     after = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     assert not torch.equal(after["enc1.block.0.weight"], edited["enc1.block.0.weight"])
     assert same(run(), fresh(after))
+
+
+def test_640x480_forward_fp32_and_bf16_vs_oracle():
+    """BASELINE config 4's resolution (640x480): the fp32 eval forward within the north star's per-pixel 1e-3 of the
+    CPU restatement, and the bf16 train-mode forward (batch statistics) within the bf16 bounds above."""
+    st = U.make_state(32, seed=3)
+    b = U.make_batch(2, 480, 640, seed=12)
+    net = U.Net(st)
+    x = torch.as_tensor(b["input"])
+    with torch.no_grad():
+        d_ev, lv_ev = net.forward(x[:1], train=False)
+        d_tr, lv_tr = net.forward(x, train=True)
+    m = _hip_model(st, 32, "fp32").eval()
+    with torch.no_grad():
+        d, lv = m(x[:1].to(DEV), return_uncertainty=True)
+    assert float((d.cpu() - d_ev).abs().max()) < 1e-3
+    assert float((lv.cpu() - lv_ev).abs().max()) < 1e-3
+    m = _hip_model(st, 32, "bf16").train()
+    with torch.no_grad():
+        d, lv = m(x.to(DEV), return_uncertainty=True)
+    for got, ref in ((d.cpu(), d_tr), (lv.cpu(), lv_tr)):
+        err = (got - ref).abs()
+        assert float((err / (1 + ref.abs())).max()) < 0.1
+        assert float(err.mean()) < 5e-3 * float(ref.abs().mean()) + 5e-3
