@@ -119,32 +119,47 @@ __global__ __launch_bounds__(256, 2) void k_heads(const T* __restrict__ y, const
     // group is px0 + u*stride, and lane `sub` owns pixel u = sub for the scalar work
     constexpr int UNR = LPP;
     const long long stride = (long long)gridDim.x * PPB;
-    for (long long px0 = blockIdx.x * (long long)PPB + threadIdx.x / LPP; px0 < P; px0 += UNR * stride) {
+    // Software-pipelined over two register sets: iteration k+1's loads are issued before iteration k's math, so
+    // two iterations of loads are in flight per lane (one left the kernel at ~4 TB/s, bytes-in-flight bound).
+    // Every iteration issues the same loads (past P: pixel 0, results dropped), none conditional.
+    struct Ld {
         uint4 raw[UNR][sizeof(T) / 2];
+        float tg, gdv, glv;
+        bool mk;
+    };
+    auto load = [&](Ld& q, long long px0) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const long long px = px0 + u * stride;
             const long long pq = px < P ? px : 0;  // tail: re-read pixel 0, results dropped below
 #pragma unroll
-            for (int h = 0; h < (int)(sizeof(T) / 2); ++h) raw[u][h] = reinterpret_cast<const uint4*>(y + pq * C + c0)[h];
+            for (int h = 0; h < (int)(sizeof(T) / 2); ++h) q.raw[u][h] = reinterpret_cast<const uint4*>(y + pq * C + c0)[h];
         }
         const long long pme = px0 + sub * stride;  // this lane's own pixel
         const bool mine = pme < P;
         const long long pmq = mine ? pme : 0;
-        float tg = 0.f, gdv = 0.f, glv_in = 0.f;
-        bool mk = false;
+        q.tg = 0.f;
+        q.gdv = 0.f;
+        q.glv = 0.f;
+        q.mk = false;
         if constexpr (MODE == SD_HEADS_LOSS) {
-            tg = target[pmq];
-            mk = mine && mask[pmq] != 0;
+            q.tg = target[pmq];
+            q.mk = mine & (mask[pmq] != 0);
         } else if constexpr (MODE == SD_HEADS_GRADS) {
-            gdv = gdisp ? gdisp[pmq] : 0.f;
-            glv_in = glogvar ? glogvar[pmq] : 0.f;
+            q.gdv = gdisp ? gdisp[pmq] : 0.f;
+            q.glv = glogvar ? glogvar[pmq] : 0.f;
         }
+    };
+    auto compute = [&](const Ld& q, long long px0) __attribute__((always_inline)) {
+        const long long pme = px0 + sub * stride;  // this lane's own pixel
+        const bool mine = pme < P;
+        const float tg = q.tg, gdv = q.gdv, glv_in = q.glv;
+        const bool mk = q.mk;
         float a[UNR][8], vd[UNR], vl[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             float yv[8];
-            raw_to_f32<T>(raw[u], yv);
+            raw_to_f32<T>(q.raw[u], yv);
             float pd = 0.f, pl = 0.f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -175,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void k_heads(const T* __restrict__ y, const
             if (disp) disp[pme] = p;
             if (logvar) logvar[pme] = lv;
         }
-        if constexpr (MODE == SD_HEADS_INFER) continue;
+        if constexpr (MODE == SD_HEADS_INFER) return;
         float gxd = 0.f, gxl = 0.f;
         if constexpr (MODE == SD_HEADS_LOSS) {
             if (mk && isfinite(tg)) {
@@ -213,7 +228,7 @@ __global__ __launch_bounds__(256, 2) void k_heads(const T* __restrict__ y, const
             if (da) store8(da + px * C + c0, o);
             if constexpr (BNSUM) {
                 float yv[8];
-                raw_to_f32<T>(raw[u], yv);
+                raw_to_f32<T>(q.raw[u], yv);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const float dz = a[u][i] > 0.f ? (float)(T)o[i] : 0.f;  // the stored da, through the ReLU mask
@@ -221,6 +236,26 @@ __global__ __launch_bounds__(256, 2) void k_heads(const T* __restrict__ y, const
                     b2[i] += dz * yv[i];  // sum dz*y; sum dz*xhat = invstd*(sum dz*y - mean*sum dz)
                 }
             }
+        }
+    };
+    const long long step = UNR * stride;
+    // the pipelined form where its second register set fits in 256 VGPRs without spilling (bf16, C <= 32 except two
+    // C = 32 instances off the training path); one set otherwise
+    constexpr bool PIPE = sizeof(T) == 2 && (C <= 16 || (C == 32 && (BNSUM || MODE == SD_HEADS_INFER)));
+    Ld qa, qb;
+    long long px0 = blockIdx.x * (long long)PPB + threadIdx.x / LPP;
+    if constexpr (PIPE) {
+        load(qa, px0);
+        for (; px0 < P; px0 += 2 * step) {
+            load(qb, px0 + step);
+            compute(qa, px0);
+            load(qa, px0 + 2 * step);
+            compute(qb, px0 + step);
+        }
+    } else {
+        for (; px0 < P; px0 += step) {
+            load(qa, px0);
+            compute(qa, px0);
         }
     }
     if constexpr (MODE == SD_HEADS_INFER) return;
