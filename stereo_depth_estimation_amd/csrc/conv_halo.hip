@@ -1172,8 +1172,10 @@ constexpr int WS_PD = 5;                        // tap-steps of fragment read-ah
 // tiles carry little MFMA work and need more loads in flight; one otherwise
 __host__ __device__ constexpr int ws_blocks_per_cu(int cout, int cib) { return cout == 32 && cib == 32 ? 2 : 1; }
 
-template <int COUT, int CIB, int HP, int HR, bool BNB>  // dy / x channels per block; halo pitch and rows (tw+2 <= HP,
-                                                       // th+2 <= HR); BNB: BatchNorm-backward apply in the dy staging
+template <int COUT, int CIB, int HP, int HR, bool BNB, bool SPAN>  // dy / x channels per block; halo pitch and
+                                                       // rows (tw+2 <= HP, th+2 <= HR); BNB: BatchNorm-backward apply
+                                                       // in the dy staging; SPAN: a block's x channels may straddle
+                                                       // the two sources of a concatenation
 __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_wgrad_ws(const HWgArgs p) {
     constexpr int KS = WS_TPX / 32;
     constexpr int NCI = CIB / 16, NCO = 4 / NCI, RM = COUT / 16 / NCO;  // wave grid and 16-row tiles per wave
@@ -1234,12 +1236,16 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             }
             hgeo[i / 2] = e[0] | e[1] << 16;
         }
-        // this thread's 8 x channels (fixed piece): their source, channel stride and BN affine (slab: any valid
-        // address). Per thread, so a block's CIB channels may span both sources of a concatenation (dec1.0: 32 + 32
-        // in one 64-channel block, whose dy transform then runs once instead of once per 32-channel block)
+        // this thread's 8 x channels (fixed piece): their BN affine (slab: any valid address), channel stride and
+        // offset. The buffer resource stays block-uniform (the source of the block's first channel): a per-lane
+        // base made hipcc wrap every halo load in a waterfall loop (+8 % on every instance). SPAN (dec1.0: 32 + 32
+        // in one 64-channel block, whose dy transform then runs once instead of once per 32-channel block): each
+        // lane loads through the resource of its own source, with the other source's load out of range
         const HaloCol hc = halo_col(p.x, cc * CIB + xpiece * 8, p.slab);
-        const __bf16* xsrc = hc.base;
-        const int xC = hc.C;
+        const bool bsrc1 = cc * CIB >= p.x.c0;
+        const __bf16* xsrc = bsrc1 ? p.x.p1 : p.x.p0;
+        const int xC = SPAN ? hc.C : (bsrc1 ? p.x.c1 : p.x.c0);  // per lane only with SPAN (offsets, not resources)
+        const bool lsrc1 = SPAN && cc * CIB + xpiece * 8 >= p.x.c0;
         // Per-piece element offsets from the tile origin (h0, w0), fixed for the launch: a piece's buffer
         // offset is then one add, its bounds test four compares against per-tile scalars, and a piece
         // outside the image / tile gets an offset past the buffer's range, which the buffer load returns
@@ -1298,8 +1304,11 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
                 q.img = b;
                 q.wr = tile % p.ncc == cc;
             }
+            const int bxC = bsrc1 ? p.x.c1 : p.x.c0;
             const __amdgpu_buffer_rsrc_t rx =
-                __builtin_amdgcn_make_buffer_rsrc((void*)(xsrc + img * xC), (short)0, nimg * xC * 2, 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc((void*)(xsrc + img * bxC), (short)0, nimg * bxC * 2, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rx1 = __builtin_amdgcn_make_buffer_rsrc(  // SPAN: source 1 (dual-source calls)
+                (void*)(SPAN ? p.x.p1 + img * p.x.c1 : xsrc), (short)0, SPAN ? nimg * p.x.c1 * 2 : 0, 0x00020000);
             // halo piece (hy, hx) is inside the image iff 1 - h0 <= hy < H - h0 + 1 and 1 - w0 <= hx < W - w0 + 1
             int rlo = 1 - h0, rhi = p.H - h0 + 1, clo = 1 - w0, chi = p.W - w0 + 1;
             if (tile >= t_begin + ntile) rhi = rlo;  // past the block's range: every piece out of range, no traffic
@@ -1331,8 +1340,14 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
                 const bool ok = (gg != 0xffffu) & (hy >= rlo) & (hy < rhi) & (hx >= clo) & (hx < chi);
                 xm |= (unsigned)ok << i;
                 const unsigned off = ok ? (unsigned)(xbase + xpo[i]) * 2u : 0x80000000u;
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-                q.x[i] = make_uint4(v[0], v[1], v[2], v[3]);
+                if constexpr (SPAN) {
+                    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rx, lsrc1 ? OOB : off, 0, 0);
+                    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rx1, lsrc1 ? off : OOB, 0, 0);
+                    q.x[i] = make_uint4(v0[0] | v1[0], v0[1] | v1[1], v0[2] | v1[2], v0[3] | v1[3]);
+                } else {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+                    q.x[i] = make_uint4(v[0], v[1], v[2], v[3]);
+                }
             }
             q.xm = xm;
         };
@@ -1795,6 +1810,7 @@ static HTile wgrad_tile(int H, int W) {
 // SD_WG_WS=0 keeps k_halo_wgrad everywhere (A/B runs).
 struct WsCfg {
     int cout, cib;
+    bool span = false;  // a block's CIB channels straddle the two sources (k_halo_wgrad_ws SPAN)
 };
 static WsCfg wgrad_ws(int M, int N, int c0 = -1) {
     static const bool on = [] {
@@ -1809,8 +1825,13 @@ static WsCfg wgrad_ws(int M, int N, int c0 = -1) {
         const char* e = getenv("SD_WS_CIB64");
         return !(e && atoi(e) == 0);
     }();
-    if (ctot % 64 == 0 && (c0 < 0 || c0 % 64 == 0 || (span && c0 % 8 == 0))) c.cib = 64;
-    else if (ctot % 32 == 0 && (c0 < 0 || c0 % 32 == 0)) c.cib = 32;
+    // the straddling (SPAN) instance is built for 32 dy channels only (dec1.0): 64 dy channels keep 32-channel x blocks
+    if (ctot % 64 == 0 && (c0 < 0 || c0 % 64 == 0 || (span && c.cout == 32 && c0 % 8 == 0))) {
+        c.cib = 64;
+        c.span = c0 > 0 && c0 % 64 != 0;
+    } else if (ctot % 32 == 0 && (c0 < 0 || c0 % 32 == 0)) {
+        c.cib = 32;
+    }
     return c.cib ? c : WsCfg{0, 0};
 }
 
@@ -1864,21 +1885,23 @@ const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W, bool bnb) {
     const WsCfg ws = wgrad_ws(M, N, c0);
     if (!ws.cib) return M == 32 ? (bnb ? "k_halo_wgrad<32, true>" : "k_halo_wgrad<32, false>") : "k_halo_wgrad<64, false>";
     const WsTile t = wgrad_tile_ws(H, W);
-    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false");
+    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s, %s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false",
+             ws.span ? "true" : "false");
     return buf;
 }
 
-template <int COUT, int CIB, bool BNB>
+template <int COUT, int CIB, bool BNB, bool SPAN = false>
 static void launch_wgrad_ws(int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
     if (hp == 34)
-        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6, BNB>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6, BNB, SPAN>), grid, dim3(512), 0, st, p);
     else
-        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8, BNB>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8, BNB, SPAN>), grid, dim3(512), 0, st, p);
 }
 template <bool BNB>
 static void launch_wgrad_ws(const WsCfg& ws, int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
     if (ws.cout == 64 && ws.cib == 64) launch_wgrad_ws<64, 64, BNB>(hp, grid, st, p);
     else if (ws.cout == 64) launch_wgrad_ws<64, 32, BNB>(hp, grid, st, p);
+    else if (ws.cib == 64 && ws.span) launch_wgrad_ws<32, 64, BNB, true>(hp, grid, st, p);
     else if (ws.cib == 64) launch_wgrad_ws<32, 64, BNB>(hp, grid, st, p);
     else launch_wgrad_ws<32, 32, BNB>(hp, grid, st, p);
 }
