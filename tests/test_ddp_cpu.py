@@ -72,7 +72,7 @@ def _worker(rank: int, world: int, port: int, cap: int, q):
         dp = DataParallel.__new__(DataParallel)
         dp.group = None
         count = torch.tensor([0 if rank == 0 else 7], dtype=torch.int32)  # rank 0 alone would skip
-        dp._allreduce_count(count)
+        dp._allreduce_count(count).wait()  # async (train_step waits after the forward)
         met = torch.tensor([1.0, 2.5, 4.0], dtype=torch.float64) * (rank + 1)
         before = met.clone()
         s = dp.sum_metrics(met)

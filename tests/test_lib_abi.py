@@ -85,7 +85,7 @@ def test_planning_queries_are_host_only():
     # BatchNorm-backward apply fused into the warp-specialised weight gradients (every 3x3 wgrad but enc1.0's)
     dy = L.make_src(ctypes.c_void_p(16), 32, 240, 320, taps=1)
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy, src, 32, 288) == 1
-    assert L.kernel_name("sd_wgrad_bnbwd_kernel_name", dy, src, 32, 288) == "k_halo_wgrad_ws<32, 32, 22, 8, true>"
+    assert L.kernel_name("sd_wgrad_bnbwd_kernel_name", dy, src, 32, 288) == "k_halo_wgrad_ws<32, 32, 22, 8, true, false>"
     x256 = L.make_src(ctypes.c_void_p(16), 256, 60, 80, taps=9)
     dy128 = L.make_src(ctypes.c_void_p(16), 128, 60, 80, taps=1)
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy128, x256, 128, 2304) == 4  # four 64-channel x blocks
