@@ -1820,10 +1820,12 @@ static WsCfg wgrad_ws(int M, int N, int c0 = -1) {
     const int ctot = N / 9;
     WsCfg c{M % 64 == 0 ? 64 : (M == 32 ? 32 : 0), 0};
     if (!on || c.cout == 0 || N % 9) return {0, 0};
-    // SD_WS_CIB64=0: 64-channel blocks only where the first source is a multiple of 64 (A/B runs)
+    // SD_WS_CIB64=1: 64-channel x blocks straddling the two sources for 32 dy channels (dec1.0's cat(32 + 32): one dy
+    // transform instead of two). Off: measured 590 us against 378 us for its two 32-channel blocks on one box
+    // (gpurun_out/sp1; one block per CU and two loads per halo piece)
     static const bool span = [] {
         const char* e = getenv("SD_WS_CIB64");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) == 1;
     }();
     // the straddling (SPAN) instance is built for 32 dy channels only (dec1.0): 64 dy channels keep 32-channel x blocks
     if (ctot % 64 == 0 && (c0 < 0 || c0 % 64 == 0 || (span && c.cout == 32 && c0 % 8 == 0))) {
