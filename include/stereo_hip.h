@@ -113,7 +113,8 @@ const char* sd_wgrad_kernel_name(int dtype, const sd_src* a, const sd_src* b, in
 /* sd_conv_gemm(SD_EPI_STORE) of a dgrad whose output `out` is the upstream gradient da of a BatchNorm layer with raw
  * output y (model.py:37,40): the same launch also writes that layer's BatchNorm-backward partial sums (what
  * sd_bn_bwd_reduce computes from da and y in a pass of its own), sd_conv_gemm_bnsum_rows() rows of float2[N],
- * for sd_bn_bwd_finalize. bf16 3x3 halo shapes: sd_conv_gemm_bnsum_ok. */
+ * for sd_bn_bwd_finalize. bf16 3x3 halo shapes and the ConvTranspose2d dgrad (4-tap sub-pixel source, model.py:67-73)
+ * where the LDS-resident-weight kernel takes it: sd_conv_gemm_bnsum_ok. */
 int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad,
                        void* out, const void* y, const float* scale, const float* shift, const float* mean,
                        const float* invstd, float* partials, sd_stream s);
