@@ -70,6 +70,15 @@ class GemmTimer:
         self.encoder = []
         self._last_phase = ""
         self._fwd_conv = 0
+        self._streams = {}
+
+    def _stream(self, handle):
+        cur = self.torch.cuda.current_stream()
+        if not handle or handle == cur.cuda_stream:
+            return cur
+        if handle not in self._streams:
+            self._streams[handle] = self.torch.cuda.ExternalStream(handle)
+        return self._streams[handle]
 
     def _flops_and_name(self, name, args):
         L, eng = self.L, self.eng
@@ -97,7 +106,7 @@ class GemmTimer:
         if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
-        ev.record()
+        ev.record(self._stream(args[-1]))  # the launch stream (SD_SIDE_REDUCE=2 puts some GEMMs on a second one)
         if phase == "pre":
             self.cur = (ev, *self._flops_and_name(name, args))
             if getattr(self.eng, "phase", "") != self._last_phase:

@@ -160,6 +160,14 @@ class UNetEngine:
         # (sd_conv_gemm_bnsum; SD_BNSUM_FUSE=0: sd_bn_bwd_reduce pass)
         self.bnsum_fuse = os.environ.get("SD_BNSUM_FUSE", "1") != "0"
         self._bnsum_rows: dict[str, int] = {}
+        # training: the split-K slab reduce of every weight gradient on a second stream (SD_SIDE_REDUCE=1), so it
+        # overlaps the next layer's kernels instead of adding a kernel boundary to the critical path; 2: the
+        # weight-gradient GEMMs that nothing downstream reads (no fused dy) on that stream too. Two slabs
+        # alternate; an event per slab orders its reuse. 0: everything on the current stream.
+        self.side_mode = int(os.environ.get("SD_SIDE_REDUCE", "0"))
+        self._side: torch.cuda.Stream | None = None
+        self._slab_free: list = [None, None]
+        self._slab_i = 0
         self.params: dict[str, torch.Tensor] = {}
         self.grads: dict[str, torch.Tensor] = {}
         self.bufs: dict[str, torch.Tensor] = {}
@@ -307,6 +315,9 @@ class UNetEngine:
             max_chan = max(max_chan, L.call("sd_heads_rows", B * H * W) * self.convs["dec1.1"].cout * 2)
             t["chan"] = torch.empty(max_chan, dtype=f32, device=dev)
             t["slab"] = torch.empty(max_slab, dtype=f32, device=dev)
+            if self.side_mode:
+                t["slab1"] = torch.empty(max_slab, dtype=f32, device=dev)
+                self._slab_free = [None, None]
             P0 = B * H * W
             t["heads_part"] = torch.empty(L.call("sd_heads_rows", P0) * (2 * self.c1 + 7), dtype=f32, device=dev)
         self.ws = ws
@@ -553,12 +564,48 @@ class UNetEngine:
                    coef.data_ptr(), P, cl.cout, t["dy:" + cl.name].data_ptr(), s)
 
     def _wgrad(self, a: L.SdSrc, b: L.SdSrc, lvl: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor):
-        ws, s, dt = self.ws, self._s(), self.sd_dtype
+        ws, dt = self.ws, self.sd_dtype
         Hl, Wl = ws.H >> lvl, ws.W >> lvl
         sp = L.call("sd_wgrad_splits", dt, ws.B, Hl, Wl, M, N)
-        slab = ws.t["slab"]
-        L.call("sd_wgrad_gemm", dt, a, b, ws.B, Hl, Wl, M, N, slab.data_ptr(), sp, s)
-        L.call("sd_wgrad_reduce", slab.data_ptr(), sp, M, N, layout, ci_real, dw.data_ptr(), s)
+        self._wgrad_slabs(lambda slab, st: L.call("sd_wgrad_gemm", dt, a, b, ws.B, Hl, Wl, M, N, slab, sp, st),
+                          sp, M, N, layout, ci_real, dw, gemm_may_side=True)
+
+    def _side_stream(self) -> torch.cuda.Stream:
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
+    def _wgrad_slabs(self, gemm, sp: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor,
+                     gemm_may_side: bool):
+        """gemm(slab_ptr, stream) writes sp split-K slabs of an M x N weight gradient; sd_wgrad_reduce sums them
+        into dw. With side_mode the reduce runs on the side stream (and with side_mode 2 a gemm_may_side GEMM too)."""
+        s = self._s()
+        if not self.side_mode:
+            slab = self.ws.t["slab"].data_ptr()
+            gemm(slab, s)
+            L.call("sd_wgrad_reduce", slab, sp, M, N, layout, ci_real, dw.data_ptr(), s)
+            return
+        main, side = torch.cuda.current_stream(self.device), self._side_stream()
+        i = self._slab_i
+        self._slab_i ^= 1
+        slab = self.ws.t["slab1" if i else "slab"].data_ptr()
+        if gemm_may_side and self.side_mode >= 2:
+            side.wait_stream(main)  # its operands (dy, x) come from the current stream; the slab's last reduce
+            gemm(slab, side.cuda_stream)  # precedes it on the side stream
+        else:
+            if self._slab_free[i] is not None:
+                main.wait_event(self._slab_free[i])  # the reduce that last read this slab
+            gemm(slab, s)
+            side.wait_stream(main)
+        L.call("sd_wgrad_reduce", slab, sp, M, N, layout, ci_real, dw.data_ptr(), side.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        self._slab_free[i] = ev
+
+    def _side_join(self):
+        """The current stream waits for everything queued on the side stream (gradients final)."""
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
 
     def _conv_bwd(self, cl: ConvL, need_dgrad: bool, fused_rows: int = 0):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
@@ -581,12 +628,13 @@ class UNetEngine:
         self._bn_bwd(cl, fused_rows, apply=not fuse)
         if fuse:
             sp = L.call("sd_wgrad_splits", dt, ws.B, Hl, Wl, M, N)
-            slab = t["slab"]
-            L.call("sd_wgrad_gemm_bnbwd", dt, a, b, ws.B, Hl, Wl, M, N, t["da:" + cl.name].data_ptr(),
-                   t["y:" + cl.name].data_ptr(), t["scale:" + cl.name].data_ptr(), t["shift:" + cl.name].data_ptr(),
-                   t["mean:" + cl.name].data_ptr(), t["invstd:" + cl.name].data_ptr(),
-                   t["coef:" + cl.name].data_ptr(), slab.data_ptr(), sp, s)
-            L.call("sd_wgrad_reduce", slab.data_ptr(), sp, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key].data_ptr(), s)
+            args = (t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), t["scale:" + cl.name].data_ptr(),
+                    t["shift:" + cl.name].data_ptr(), t["mean:" + cl.name].data_ptr(),
+                    t["invstd:" + cl.name].data_ptr(), t["coef:" + cl.name].data_ptr())
+            # writes dy, which the dgrad below reads: stays on the current stream
+            self._wgrad_slabs(lambda slab, st: L.call("sd_wgrad_gemm_bnbwd", dt, a, b, ws.B, Hl, Wl, M, N, *args,
+                                                      slab, sp, st),
+                              sp, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key], gemm_may_side=False)
         if need_dgrad:
             dsrc = L.make_src(dy, cl.cout, Hl, Wl, taps=9)
             if cl.idx == 1:
@@ -680,11 +728,24 @@ class UNetEngine:
             self._conv_bwd(self.convs[blk + ".0"], need_dgrad=(blk != "enc1"),
                            fused_rows=self._bnsum_rows.pop(blk + ".0", 0))
             if grad_hook is not None:
-                grad_hook(blk)
+                self._grads_ready(grad_hook, blk)
             if blk in UP_OF_DEC:
                 self._up_bwd(self.ups[UP_OF_DEC[blk]])
                 if grad_hook is not None:
-                    grad_hook(UP_OF_DEC[blk])
+                    self._grads_ready(grad_hook, UP_OF_DEC[blk])
+        self._side_join()
+
+    def _grads_ready(self, grad_hook, name: str):
+        """grad_hook(name) with the current stream at a point where `name`'s gradients are final. With side-stream
+        reduces that is the side stream once it has caught up with this one: a collective the hook launches then
+        waits for the reduces without the current stream waiting for them."""
+        if self._side is None:
+            grad_hook(name)
+            return
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            grad_hook(name)
 
     def adamw(self, flat_p, flat_g, m, v, lr, weight_decay, betas=(0.9, 0.999), eps=1e-8, gate_on_count=True):
         self.touch_state()

@@ -200,6 +200,27 @@ def test_full_size_train_step_bf16_grads(golden_dir, _bn_fuse_env):
         assert e_fused <= max(1.5 * e_sep, 2e-2), (k, e_fused, e_sep)
 
 
+@pytest.mark.parametrize("side", [1, 2])
+def test_side_stream_reduces_bit_identical(monkeypatch, side):
+    """SD_SIDE_REDUCE=1/2 (slab reduces, and unfused weight-gradient GEMMs, on a second stream with a two-slab
+    ring) only reorders independent launches: gradients, metrics and updated weights equal the one-stream run
+    exactly, over two steps (the second step reuses both slabs under the events of the first)."""
+    st = U.make_state(32, seed=3)
+    bs = [U.make_batch(2, 96, 128, seed=6), U.make_batch(2, 96, 128, seed=7)]
+    runs = {}
+    for mode in (0, side):
+        monkeypatch.setenv("SD_SIDE_REDUCE", str(mode))
+        m, metrics, _, grads = _fused_two_steps(st, 32, "bf16", bs)
+        assert m.engine().side_mode == mode
+        torch.cuda.synchronize()
+        runs[mode] = (metrics, grads, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()})
+    assert runs[0][0] == runs[side][0]
+    for k, g0 in runs[0][1].items():
+        assert torch.equal(g0, runs[side][1][k]), k
+    for k, p0 in runs[0][2].items():
+        assert torch.equal(p0, runs[side][2][k]), k
+
+
 def test_autograd_path_matches_fused_path():
     """model(x) + external loss + loss.backward() (the reference's train.py:328-342 as written)."""
     st = U.make_state(8, seed=0, signed_gamma=True)
