@@ -296,11 +296,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # SD_BENCH_SHARE_DEVICE=1: every rank on cuda:0 over gloo, a rehearsal of the N > 1 path (buckets, count
+    # all-reduce, barriers, max-over-ranks timing) on a one-GPU box; its rate is not a scaling number
+    share = world > 1 and os.environ.get("SD_BENCH_SHARE_DEVICE", "0") == "1"
+    if share:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from stereo_depth_estimation_amd import _lib as L
@@ -386,6 +394,8 @@ def main():
             "parallelism": f"dp{world}",
         },
     }
+    if share:
+        result["rehearsal"] = f"gloo, {world} ranks sharing cuda:0 (SD_BENCH_SHARE_DEVICE=1): not a scaling number"
     peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
     step_tflops = TRAIN_GFLOP_PER_PAIR * 1e9 * B * (H * W) / (240 * 320) / (dt / args.steps) / 1e12
     result["step_conv_tflops"] = round(step_tflops, 2)
