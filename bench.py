@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-infer", action="store_true", help="skip the 960x720 fp8/bf16/fp32 inference lines")
+    ap.add_argument("--sync-bn", action="store_true", help="N > 1: global-batch BatchNorm statistics (SyncBatchNorm)")
     return ap.parse_args()
 
 
@@ -324,7 +325,7 @@ def main():
     if world > 1:
         from stereo_depth_estimation_amd.ddp import DataParallel
 
-        ddp = DataParallel(model)
+        ddp = DataParallel(model, sync_bn=args.sync_bn)
     B, H, W = args.batch, args.height, args.width
     ring = [synthetic_batch(B, H, W, seed=1000 * rank + i, device=dev) for i in range(4)]
     log(f"rank {rank}/{world}: model + {len(ring)} resident batches of {B}x6x{H}x{W} ready")
@@ -392,6 +393,7 @@ def main():
             "height": H,
             "width": W,
             "parallelism": f"dp{world}",
+            "batchnorm": "sync" if (args.sync_bn and world > 1) else "per-rank",
         },
     }
     if share:

@@ -79,6 +79,7 @@ class TrainConfig:  # reference train.py:38-58, plus the HIP path's options at t
     blur_kernel_size: int
     resume: str | None = None
     precision: str = "bf16"
+    sync_bn: bool = False
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -116,6 +117,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--blur-kernel-size", type=int, default=5)
     p.add_argument("--resume", type=str, default=None, help="Checkpoint (last.pt) to continue from.")
     p.add_argument("--precision", type=str, default="bf16", choices=("bf16", "fp32"))
+    p.add_argument("--sync-bn", action="store_true",
+                   help="multi-GPU: BatchNorm statistics over the global batch (SyncBatchNorm) instead of per rank")
     return p
 
 
@@ -294,7 +297,7 @@ def main(argv=None) -> dict:
         if rank == 0:
             print(f"Resumed from {args.resume}: epoch {start_epoch - 1}, global step {global_step}")
     if world > 1:
-        ddp = DataParallel(model)
+        ddp = DataParallel(model, sync_bn=args.sync_bn)
 
     # run directory and logger (MLflow when available, else JSON lines)
     logger, run_ctx, run_id = _NullLogger(), None, args.run_name or time.strftime("run-%Y%m%d-%H%M%S")

@@ -26,6 +26,29 @@ __device__ __forceinline__ void block_sum2(double& a, double& b) {
     b = red[1][0];
 }
 
+// mean/invstd/scale/shift and the running-statistics update of channel c from its fp64 (sum, sumsq) over `count`
+// pixels (every rank's, with SyncBatchNorm: the unbiased variance then uses the global count, as torch's)
+__device__ __forceinline__ void bn_fwd_emit(int c, double s, double ss, double count, const float* gamma,
+                                            const float* beta, float* running_mean, float* running_var, int64_t* nbt,
+                                            float momentum, float eps, float* mean_o, float* invstd_o, float* scale_o,
+                                            float* shift_o) {
+    const double mean = s / count;
+    double var = ss / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * invstd;
+    mean_o[c] = (float)mean;
+    invstd_o[c] = invstd;
+    scale_o[c] = sc;
+    shift_o[c] = beta[c] - (float)mean * sc;
+    if (running_mean) {
+        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        running_mean[c] = (float)(momentum * mean + (1.0 - momentum) * (double)running_mean[c]);
+        running_var[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)running_var[c]);
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+}
+
 __global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restrict__ stats, int rows, int C,
                                                          double count, const float* gamma, const float* beta,
                                                          float* running_mean, float* running_var, int64_t* nbt,
@@ -39,23 +62,37 @@ __global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restric
         ss += v.y;
     }
     block_sum2<256>(s, ss);
-    if (threadIdx.x == 0) {
-        const double mean = s / count;
-        double var = ss / count - mean * mean;
-        if (var < 0.0) var = 0.0;
-        const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-        const float sc = gamma[c] * invstd;
-        mean_o[c] = (float)mean;
-        invstd_o[c] = invstd;
-        scale_o[c] = sc;
-        shift_o[c] = beta[c] - (float)mean * sc;
-        if (running_mean) {
-            const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-            running_mean[c] = (float)(momentum * mean + (1.0 - momentum) * (double)running_mean[c]);
-            running_var[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)running_var[c]);
-        }
-        if (nbt && c == 0) nbt[0] += 1;
+    if (threadIdx.x == 0)
+        bn_fwd_emit(c, s, ss, count, gamma, beta, running_mean, running_var, nbt, momentum, eps, mean_o, invstd_o,
+                    scale_o, shift_o);
+}
+
+// SyncBatchNorm: the float2 partial rows of one rank -> fp64 per-channel sums[2c], sums[2c+1] (the same fixed-order
+// reduction the finalizes run), which the host all-reduces across ranks before the *_finalize64 kernels
+__global__ __launch_bounds__(256) void k_rows_sum64(const float2* __restrict__ rows_, int rows, int C, double* sums) {
+    const int c = blockIdx.x;
+    double s = 0.0, ss = 0.0;
+    for (int r = threadIdx.x; r < rows; r += 256) {
+        const float2 v = rows_[(size_t)r * C + c];
+        s += v.x;
+        ss += v.y;
     }
+    block_sum2<256>(s, ss);
+    if (threadIdx.x == 0) {
+        sums[2 * c] = s;
+        sums[2 * c + 1] = ss;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bn_fwd_finalize64(const double* __restrict__ sums, int C, double count,
+                                                           const float* gamma, const float* beta, float* running_mean,
+                                                           float* running_var, int64_t* nbt, float momentum, float eps,
+                                                           float* mean_o, float* invstd_o, float* scale_o,
+                                                           float* shift_o) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < C)
+        bn_fwd_emit(c, sums[2 * c], sums[2 * c + 1], count, gamma, beta, running_mean, running_var, nbt, momentum, eps,
+                    mean_o, invstd_o, scale_o, shift_o);
 }
 
 __global__ void k_bn_eval_coeffs(const float* rm, const float* rv, const float* gamma, const float* beta, int C,
@@ -143,6 +180,18 @@ __global__ __launch_bounds__(256) void k_chan_reduce(const ChanArgs a) {
     }
 }
 
+// dgamma/dbeta from this rank's sums (the gradient all-reduce adds the ranks' shares), coef from the sums over
+// `count` pixels (with SyncBatchNorm every rank's: gs/gss and count are global)
+__device__ __forceinline__ void bn_bwd_emit(int c, double s, double ss, double gs, double gss, double count,
+                                            const float* gamma, const float* invstd, int batch_stats, float* dgamma,
+                                            float* dbeta, float* coef) {
+    dbeta[c] = (float)s;
+    dgamma[c] = (float)ss;
+    coef[3 * c + 0] = gamma[c] * invstd[c];
+    coef[3 * c + 1] = batch_stats ? (float)(gs / count) : 0.f;
+    coef[3 * c + 2] = batch_stats ? (float)(gss / count) : 0.f;
+}
+
 __global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restrict__ part, int rows, int C,
                                                          double count, const float* gamma, const float* invstd,
                                                          int batch_stats, float* dgamma, float* dbeta, float* coef) {
@@ -154,13 +203,17 @@ __global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restric
         ss += v.y;
     }
     block_sum2<256>(s, ss);
-    if (threadIdx.x == 0) {
-        dbeta[c] = (float)s;
-        dgamma[c] = (float)ss;
-        coef[3 * c + 0] = gamma[c] * invstd[c];
-        coef[3 * c + 1] = batch_stats ? (float)(s / count) : 0.f;
-        coef[3 * c + 2] = batch_stats ? (float)(ss / count) : 0.f;
-    }
+    if (threadIdx.x == 0) bn_bwd_emit(c, s, ss, s, ss, count, gamma, invstd, batch_stats, dgamma, dbeta, coef);
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_finalize64(const double* __restrict__ local,
+                                                           const double* __restrict__ global, int C, double count,
+                                                           const float* gamma, const float* invstd, int batch_stats,
+                                                           float* dgamma, float* dbeta, float* coef) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < C)
+        bn_bwd_emit(c, local[2 * c], local[2 * c + 1], global[2 * c], global[2 * c + 1], count, gamma, invstd,
+                    batch_stats, dgamma, dbeta, coef);
 }
 
 __global__ __launch_bounds__(256) void k_sum_finalize(const float2* __restrict__ part, int rows, int ld, float* out) {
@@ -331,6 +384,34 @@ extern "C" int sd_bn_fwd_finalize(const float* stats, int rows, int C, double co
                        gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, mean, invstd, scale,
                        shift);
     return sd_check_launch("sd_bn_fwd_finalize");
+}
+
+extern "C" int sd_bn_rows_sum64(const float* rows, int nrows, int C, double* sums, sd_stream s) {
+    SD_REQUIRE(rows && sums && nrows > 0 && C > 0, "sd_bn_rows_sum64: bad args");
+    hipLaunchKernelGGL(k_rows_sum64, dim3(C), dim3(256), 0, to_stream(s), (const float2*)rows, nrows, C, sums);
+    return sd_check_launch("sd_bn_rows_sum64");
+}
+
+extern "C" int sd_bn_fwd_finalize64(const double* sums, int C, double count, const float* gamma, const float* beta,
+                                    float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                                    float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
+                                    sd_stream s) {
+    SD_REQUIRE(sums && C > 0 && count > 0 && gamma && beta && mean && invstd && scale && shift,
+               "sd_bn_fwd_finalize64: bad args");
+    SD_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "sd_bn_fwd_finalize64: running stats pair");
+    hipLaunchKernelGGL(k_bn_fwd_finalize64, dim3(cdiv(C, 256)), dim3(256), 0, to_stream(s), sums, C, count, gamma, beta,
+                       running_mean, running_var, num_batches_tracked, momentum, eps, mean, invstd, scale, shift);
+    return sd_check_launch("sd_bn_fwd_finalize64");
+}
+
+extern "C" int sd_bn_bwd_finalize64(const double* local_sums, const double* global_sums, int C, double count,
+                                    const float* gamma, const float* invstd, int batch_stats, float* dgamma,
+                                    float* dbeta, float* coef, sd_stream s) {
+    SD_REQUIRE(local_sums && global_sums && C > 0 && count > 0 && gamma && invstd && dgamma && dbeta && coef,
+               "sd_bn_bwd_finalize64: bad args");
+    hipLaunchKernelGGL(k_bn_bwd_finalize64, dim3(cdiv(C, 256)), dim3(256), 0, to_stream(s), local_sums, global_sums, C,
+                       count, gamma, invstd, batch_stats, dgamma, dbeta, coef);
+    return sd_check_launch("sd_bn_bwd_finalize64");
 }
 
 extern "C" int sd_bn_eval_coeffs(const float* running_mean, const float* running_var, const float* gamma,

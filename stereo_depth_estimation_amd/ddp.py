@@ -12,7 +12,9 @@ reference on the global batch:
     drift apart per rank during an epoch; ``sync_buffers()`` broadcasts rank 0's before every
     evaluation epoch and checkpoint (torch DDP's broadcast_buffers, once per epoch instead of per
     forward: nothing reads them between training forwards), so every rank evaluates, and
-    best.pt is chosen, with the statistics that are saved.
+    best.pt is chosen, with the statistics that are saved. ``sync_bn=True`` instead normalises with
+    the global batch's statistics (SyncBatchNorm: two fp64 all-reduces per BN layer per step), which
+    reproduces the single-process reference on the concatenated batch.
 Gradient buckets are contiguous slices of the flat gradient buffer (the model stores
 parameters in backward-production order), each all-reduced asynchronously on RCCL's stream
 as soon as backward finalises its last module — the collective overlaps the rest of
@@ -73,13 +75,21 @@ class BucketAllReduce:
 
 
 class DataParallel:
-    def __init__(self, model, group=None, bucket_cap_mb: float = 8.0, broadcast: bool = True):
+    def __init__(self, model, group=None, bucket_cap_mb: float = 8.0, broadcast: bool = True, sync_bn: bool = False):
+        """sync_bn: global-batch BatchNorm statistics (torch.nn.SyncBatchNorm semantics; SURVEY §8e "--sync-bn"):
+        one fp64 all-reduce of per-channel (sum, sumsq) per BN layer in the forward and of (sum dz, sum dz*xhat) in
+        the backward, 2 x 18 small collectives per step. Needs equal batch shapes on every rank."""
         self.model, self.group = model, group
         self.world = dist.get_world_size(group)
         self.cap = int(bucket_cap_mb * 1024 * 1024 / 4)
         self._ar = None
+        self.sync_bn = sync_bn
         if broadcast:
             self.broadcast_state()
+        if sync_bn:
+            eng = model.engine(next(model.parameters()).device)
+            eng.bn_sync = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            eng.bn_world = self.world
 
     def broadcast_state(self):
         dev = next(self.model.parameters()).device

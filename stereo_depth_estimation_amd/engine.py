@@ -168,6 +168,11 @@ class UNetEngine:
         self._side: torch.cuda.Stream | None = None
         self._slab_free: list = [None, None]
         self._slab_i = 0
+        # SyncBatchNorm (ddp.DataParallel(sync_bn=True)): bn_sync(t) SUM-all-reduces an fp64 device tensor in stream
+        # order; bn_world ranks with equal per-rank batch shapes. None: per-rank BatchNorm statistics.
+        self.bn_sync = None
+        self.bn_world = 1
+        self._bn64: torch.Tensor | None = None
         self.params: dict[str, torch.Tensor] = {}
         self.grads: dict[str, torch.Tensor] = {}
         self.bufs: dict[str, torch.Tensor] = {}
@@ -364,9 +369,15 @@ class UNetEngine:
             rows = L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cout)
             rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
             nbt = self.bufs.get(cl.bn_key + ".num_batches_tracked")
-            L.call("sd_bn_fwd_finalize", stats.data_ptr(), rows, cl.cout, float(ws.B * Hl * Wl), g.data_ptr(),
-                   b.data_ptr(), rm.data_ptr(), rv.data_ptr(), L.ptr(nbt), BN_MOMENTUM, BN_EPS, mean.data_ptr(),
-                   invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
+            if self.bn_sync is not None:  # global batch statistics (torch SyncBatchNorm)
+                sums = self._sync_sums(stats, rows, cl.cout)[0]
+                L.call("sd_bn_fwd_finalize64", sums.data_ptr(), cl.cout, float(ws.B * Hl * Wl * self.bn_world),
+                       g.data_ptr(), b.data_ptr(), rm.data_ptr(), rv.data_ptr(), L.ptr(nbt), BN_MOMENTUM, BN_EPS,
+                       mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
+            else:
+                L.call("sd_bn_fwd_finalize", stats.data_ptr(), rows, cl.cout, float(ws.B * Hl * Wl), g.data_ptr(),
+                       b.data_ptr(), rm.data_ptr(), rv.data_ptr(), L.ptr(nbt), BN_MOMENTUM, BN_EPS, mean.data_ptr(),
+                       invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
         else:
             L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STORE,
                    y.data_ptr(), None, 0, None, None, s)
@@ -555,13 +566,36 @@ class UNetEngine:
                    cl.cout, chan.data_ptr(), s)
             rows = L.call("sd_chan_reduce_rows", P, cl.cout)
         coef = t["coef:" + cl.name]
-        L.call("sd_bn_bwd_finalize", chan.data_ptr(), rows, cl.cout, float(P),
-               self.params[cl.bn_key + ".weight"].data_ptr(), t["invstd:" + cl.name].data_ptr(),
-               int(ws.fwd_train), self.grads[cl.bn_key + ".weight"].data_ptr(), self.grads[cl.bn_key + ".bias"].data_ptr(),
-               coef.data_ptr(), s)
+        if self.bn_sync is not None and ws.fwd_train:
+            loc, glob = self._sync_sums(chan, rows, cl.cout, keep_local=True)
+            L.call("sd_bn_bwd_finalize64", loc.data_ptr(), glob.data_ptr(), cl.cout, float(P * self.bn_world),
+                   self.params[cl.bn_key + ".weight"].data_ptr(), t["invstd:" + cl.name].data_ptr(), 1,
+                   self.grads[cl.bn_key + ".weight"].data_ptr(), self.grads[cl.bn_key + ".bias"].data_ptr(),
+                   coef.data_ptr(), s)
+        else:
+            L.call("sd_bn_bwd_finalize", chan.data_ptr(), rows, cl.cout, float(P),
+                   self.params[cl.bn_key + ".weight"].data_ptr(), t["invstd:" + cl.name].data_ptr(),
+                   int(ws.fwd_train), self.grads[cl.bn_key + ".weight"].data_ptr(),
+                   self.grads[cl.bn_key + ".bias"].data_ptr(), coef.data_ptr(), s)
         if apply:
             L.call("sd_bn_bwd_apply", dt, t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), *args,
                    coef.data_ptr(), P, cl.cout, t["dy:" + cl.name].data_ptr(), s)
+
+    def _sync_sums(self, rows_t: torch.Tensor, rows: int, C: int, keep_local: bool = False):
+        """SyncBatchNorm: this rank's float2 partial rows -> fp64 per-channel sums, SUM-all-reduced over the ranks
+        (stream-ordered). Returns (global, _) or, with keep_local, (local, global)."""
+        if C > 2048:
+            raise ValueError(f"SyncBatchNorm: {C} channels > 2048")
+        if self._bn64 is None or self._bn64.device != self.device:
+            self._bn64 = torch.empty(2, 2 * 2048, dtype=torch.float64, device=self.device)
+        loc, glob = self._bn64[0, :2 * C], self._bn64[1, :2 * C]
+        L.call("sd_bn_rows_sum64", rows_t.data_ptr(), rows, C, loc.data_ptr(), self._s())
+        if not keep_local:
+            self.bn_sync(loc)
+            return loc, None
+        glob.copy_(loc)
+        self.bn_sync(glob)
+        return loc, glob
 
     def _wgrad(self, a: L.SdSrc, b: L.SdSrc, lvl: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor):
         ws, dt = self.ws, self.sd_dtype

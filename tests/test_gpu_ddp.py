@@ -122,3 +122,73 @@ def test_ddp_two_ranks_match_single_process_and_skip_globally(backend):
         assert moved, f"rank {rank}: zero-local-valid rank skipped the step (skip must use the global count)"
         assert in_sync, f"rank {rank}: ranks diverged, or BN buffers not re-synced by sync_buffers()"
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _sync_bn_worker(rank: int, world: int, port: int, q):
+    import torch.distributed as dist
+
+    from stereo_depth_estimation_amd.data import synthetic_batch
+    from stereo_depth_estimation_amd.ddp import DataParallel
+    from stereo_depth_estimation_amd.model import StereoUNet
+    from stereo_depth_estimation_amd.optim import FusedAdamW
+    from stereo_depth_estimation_amd.train import train_step
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def make():
+            torch.manual_seed(0)
+            m = StereoUNet(in_channels=6, out_channels=1, base_channels=8, precision="fp32").to(dev)
+            return m, FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+
+        b = synthetic_batch(2 * world, 32, 48, seed=21, device=dev)
+        shard = {k: v[2 * rank:2 * rank + 2] for k, v in b.items()}
+        m_ref, o_ref = make()
+        train_step(m_ref, o_ref, b["input"], b["target"], b["valid_mask"])  # one process, the whole batch
+        g_ref = m_ref.flat_buffers()[1].double().clone()
+        bufs_ref = [t.detach().double().clone() for t in m_ref.buffers()]
+        out = {}
+        for sync in (True, False):  # sync-BN, and per-rank BN as the control the test must tell apart
+            m, o = make()
+            dp = DataParallel(m, bucket_cap_mb=0.05, sync_bn=sync)
+            dp.step(m, o, shard["input"], shard["target"], shard["valid_mask"])
+            torch.cuda.synchronize()
+            g = m.flat_buffers()[1].double()
+            rel = float((g - g_ref).norm() / g_ref.norm())
+            bd = max(float((t.detach().double() - r).abs().max()) for t, r in zip(m.buffers(), bufs_ref))
+            out[sync] = (rel, bd)
+        diff, bdiff = out[True]
+        ctrl = out[False][0]
+        q.put((rank, diff, bdiff, ctrl, None))
+    except Exception as e:
+        q.put((rank, None, None, None, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_bn_two_ranks_match_single_process_on_the_global_batch():
+    """DataParallel(sync_bn=True): two ranks on half a batch each normalise with the global batch's BatchNorm
+    statistics, so the all-reduced gradient of one step equals the single-process gradient on the whole batch (the
+    reference's semantics) within fp32 rounding, and so do the BN running statistics (incl. the unbiased variance
+    over the global count). Per-rank BN on the same shards is the control: its gradient must be far off."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_bn_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+    for rank, diff, bdiff, ctrl, err in results:
+        assert err is None, f"rank {rank}: {err}"
+        assert diff <= 1e-5, f"rank {rank}: sync-BN gradient differs from the single-process global batch by {diff} (rel)"
+        assert bdiff <= 1e-5, f"rank {rank}: sync-BN running statistics differ by {bdiff}"
+        assert ctrl > 100 * diff, f"rank {rank}: per-rank BN ({ctrl}) not distinguishable from sync-BN ({diff})"
+    assert all(p.exitcode == 0 for p in procs)
