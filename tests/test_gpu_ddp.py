@@ -94,7 +94,7 @@ def _worker(rank: int, world: int, port: int, q, backend: str = "gloo"):
         synced = all(torch.equal(gathered[0], g) for g in gathered)
         q.put((rank, diff, moved, in_sync and drifted and synced, None))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, None, None, None, repr(e)))
+        q.put((rank, None, None, None, None, repr(e)))
         raise
     finally:
         dist.destroy_process_group()
@@ -124,7 +124,7 @@ def test_ddp_two_ranks_match_single_process_and_skip_globally(backend):
     assert all(p.exitcode == 0 for p in procs)
 
 
-def _sync_bn_worker(rank: int, world: int, port: int, q):
+def _sync_bn_worker(rank: int, world: int, port: int, q, precision: str = "fp32"):
     import torch.distributed as dist
 
     from stereo_depth_estimation_amd.data import synthetic_batch
@@ -140,10 +140,13 @@ def _sync_bn_worker(rank: int, world: int, port: int, q):
     try:
         def make():
             torch.manual_seed(0)
-            m = StereoUNet(in_channels=6, out_channels=1, base_channels=8, precision="fp32").to(dev)
+            m = StereoUNet(in_channels=6, out_channels=1, base_channels=base, precision=precision).to(dev)
             return m, FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
 
-        b = synthetic_batch(2 * world, 32, 48, seed=21, device=dev)
+        # fp32: the small parity configuration; bf16: the product kernels (halo convs, fused BN-backward sums from
+        # the pool backward / dgrad epilogues / heads, all feeding the synced finalizes)
+        base, H, W = (8, 32, 48) if precision == "fp32" else (32, 64, 96)
+        b = synthetic_batch(2 * world, H, W, seed=21, device=dev)
         shard = {k: v[2 * rank:2 * rank + 2] for k, v in b.items()}
         m_ref, o_ref = make()
         train_step(m_ref, o_ref, b["input"], b["target"], b["valid_mask"])  # one process, the whole batch
@@ -157,38 +160,49 @@ def _sync_bn_worker(rank: int, world: int, port: int, q):
             torch.cuda.synchronize()
             g = m.flat_buffers()[1].double()
             rel = float((g - g_ref).norm() / g_ref.norm())
-            bd = max(float((t.detach().double() - r).abs().max()) for t, r in zip(m.buffers(), bufs_ref))
+            bd = max(float((t.detach().double() - r).abs().max() / (r.abs().max() + 1e-12))
+                     for t, r in zip(m.buffers(), bufs_ref) if t.is_floating_point())
             out[sync] = (rel, bd)
         diff, bdiff = out[True]
-        ctrl = out[False][0]
-        q.put((rank, diff, bdiff, ctrl, None))
+        ctrl, bctrl = out[False]
+        print(f"sync-bn {precision} rank {rank}: grad rel {diff:.3e} (per-rank BN {ctrl:.3e}), "
+              f"running stats rel {bdiff:.3e} (per-rank BN {bctrl:.3e})", flush=True)
+        q.put((rank, diff, bdiff, ctrl, bctrl, None))
     except Exception as e:
-        q.put((rank, None, None, None, repr(e)))
+        q.put((rank, None, None, None, None, repr(e)))
         raise
     finally:
         dist.destroy_process_group()
 
 
-def test_sync_bn_two_ranks_match_single_process_on_the_global_batch():
+# bound on (gradient rel. error, running-statistics rel. error) against the single process on the whole batch
+SYNC_TOL = {"fp32": (1e-5, 1e-5), "bf16": (5e-3, 1e-5)}  # measured: 3.6e-7 / 4.0e-7, 5.0e-4 / 0
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_sync_bn_two_ranks_match_single_process_on_the_global_batch(precision):
     """DataParallel(sync_bn=True): two ranks on half a batch each normalise with the global batch's BatchNorm
     statistics, so the all-reduced gradient of one step equals the single-process gradient on the whole batch (the
     reference's semantics) within fp32 rounding, and so do the BN running statistics (incl. the unbiased variance
-    over the global count). Per-rank BN on the same shards is the control: its gradient must be far off."""
+    over the global count). Per-rank BN on the same shards is the control: it must be far off. bf16: bf16 storage of
+    every activation and gradient rounds differently when the batch is split, hence the looser bounds."""
     import torch.multiprocessing as mp
 
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sync_bn_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sync_bn_worker, args=(r, world, port, q, precision)) for r in range(world)]
     for p in procs:
         p.start()
     results = sorted(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=120)
-    for rank, diff, bdiff, ctrl, err in results:
+    gtol, btol = SYNC_TOL[precision]
+    for rank, diff, bdiff, ctrl, bctrl, err in results:
         assert err is None, f"rank {rank}: {err}"
-        assert diff <= 1e-5, f"rank {rank}: sync-BN gradient differs from the single-process global batch by {diff} (rel)"
-        assert bdiff <= 1e-5, f"rank {rank}: sync-BN running statistics differ by {bdiff}"
-        assert ctrl > 100 * diff, f"rank {rank}: per-rank BN ({ctrl}) not distinguishable from sync-BN ({diff})"
+        assert diff <= gtol, f"rank {rank}: sync-BN gradient differs from the single-process global batch by {diff} (rel)"
+        assert bdiff <= btol, f"rank {rank}: sync-BN running statistics differ by {bdiff} (rel)"
+        assert bctrl > 1e3 * btol, f"rank {rank}: per-rank BN stats ({bctrl}) not distinguishable from sync-BN"
+        assert ctrl > 10 * gtol, f"rank {rank}: per-rank BN ({ctrl}) not distinguishable from sync-BN ({diff})"
     assert all(p.exitcode == 0 for p in procs)
