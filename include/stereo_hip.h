@@ -148,6 +148,13 @@ const char* sd_wgrad_bnbwd_kernel_name(const sd_src* a, const sd_src* b, int M, 
  *   SD_W_CONVT: M = ci, N = 4*co     -> dw[ci][co][2][2] */
 int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw, sd_stream s);
 
+/* ---- host data path: the reference's sample cache (dataset.py:86-105 load_cached_sample; cache.py:50-112) ----
+ * Reads n np.savez cache files (stored zip of left.npy / right.npy uint8 [H][W][3], disparity.npy f16 [H][W]) with
+ * `threads` host threads into left/right [n][H][W][3] and disparity [n][H][W] (f16 bits). Returns 0, or 1 + the index
+ * of the first file that is missing, compressed, or of another dtype/shape (message in err), or -1 for bad args. */
+int sd_read_cache_batch(const char* const* paths, int n, int H, int W, uint8_t* left, uint8_t* right,
+                        uint16_t* disparity, int threads, char* err, int errlen);
+
 /* ---- BatchNorm2d train/eval (model.py:37,40; native_batch_norm / _backward) ---- */
 int sd_bn_fwd_finalize(const float* stats, int rows, int C, double count, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,

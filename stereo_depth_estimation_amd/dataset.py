@@ -22,8 +22,11 @@ generator state than the reference's.
 
 from __future__ import annotations
 
+import ctypes
 import hashlib
+import os
 import random
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Iterable
@@ -274,6 +277,29 @@ def save_cached_sample(cache_file: Path, left: np.ndarray, right: np.ndarray, ta
     np.savez(cache_file, left=lnp, right=rnp, disparity=target[0].astype(np.float16))
 
 
+def read_cache_batch(paths, image_size: tuple[int, int], left: torch.Tensor, right: torch.Tensor, disparity: torch.Tensor,
+                     threads: int = 16) -> None:
+    """Native (``sd_read_cache_batch``) read of reference-format cache files (``load_cached_sample``, reference
+    ``dataset.py:86-105``) into host tensors: left/right uint8 [n,H,W,3], disparity int16 [n,H,W] (the f16 bits).
+    A host thread pool inside the call, the GIL released (ctypes); no worker processes, no pickling."""
+    H, W = image_size
+    n = len(paths)
+    for t, shape, dt in ((left, (n, H, W, 3), torch.uint8), (right, (n, H, W, 3), torch.uint8),
+                         (disparity, (n, H, W), torch.int16)):
+        if tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous() or t.device.type != "cpu":
+            raise ValueError(f"read_cache_batch: expected a contiguous CPU {dt} tensor of {shape}, got {t.dtype} "
+                             f"{tuple(t.shape)}")
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(str(p)) for p in paths])
+    err = ctypes.create_string_buffer(1024)
+    rc = L.load().sd_read_cache_batch(ctypes.cast(arr, ctypes.c_void_p), n, H, W, left.data_ptr(), right.data_ptr(),
+                                      disparity.data_ptr(), threads, err, len(err))
+    if rc != 0:
+        msg = err.value.decode(errors="replace")
+        if rc > 0 and not Path(paths[rc - 1]).exists():
+            raise FileNotFoundError(f"Required cache entry not found: {msg}")
+        raise ValueError(f"Cache entry is invalid or shape-mismatched: {msg}")
+
+
 class DeviceLoader:
     """Iterates device batch dicts ``{"input","target","valid_mask"}`` for ``run_epoch``.
 
@@ -286,8 +312,17 @@ class DeviceLoader:
 
     def __init__(self, dataset: FoundationStereoDataset, batch_size: int, shuffle: bool = False, num_workers: int = 0,
                  device: torch.device | str = "cuda", drop_last: bool = False, persistent_workers: bool = False,
-                 generator: torch.Generator | None = None, sampler=None):
+                 generator: torch.Generator | None = None, sampler=None, native: bool | None = None,
+                 read_threads: int = 16):
+        """native: read batches with the in-process native cache reader (``read_cache_batch``) instead of DataLoader
+        worker processes. Default (None): on for datasets served entirely from the cache (require_cache) without
+        augmentation, the case it covers; same batch order (the DataLoader's own batch sampler) and bytes."""
         self.dataset = dataset
+        if native is None:
+            native = dataset.cache_root is not None and dataset.require_cache and not dataset.augment
+        if native and (dataset.cache_root is None or dataset.augment):
+            raise ValueError("DeviceLoader(native=True) needs a cache_root and augment=False")
+        self.native, self.read_threads = native, read_threads
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError(f"DeviceLoader prepares batches with HIP kernels; got device {self.device}")
@@ -345,17 +380,60 @@ class DeviceLoader:
                 val[g["index"].to(dev)] = gv
         return {"input": inp, "target": tgt, "valid_mask": val}
 
+    def _native_groups(self):
+        """Host batches from the native reader, in collate_uint8's format: a one-thread executor reads batch i+1 into
+        one of two pinned buffer sets while batch i is copied and prepared; a set is refilled only after the
+        event of its last H2D copy (recorded by __iter__ in self._h2d_done) has completed."""
+        H, W = self.dataset.image_size
+        root, samples = self.dataset.cache_root, self.dataset.samples
+        bmax = self.loader.batch_size
+
+        def alloc():
+            return (torch.empty(bmax, H, W, 3, dtype=torch.uint8).pin_memory(),
+                    torch.empty(bmax, H, W, 3, dtype=torch.uint8).pin_memory(),
+                    torch.empty(bmax, H, W, dtype=torch.int16).pin_memory())
+
+        bufs = [alloc(), alloc()]
+        self._h2d_done = [None, None]
+
+        def read(k, idxs):
+            n = len(idxs)
+            left, right, disp = (t[:n] for t in bufs[k])
+            read_cache_batch([root / sample_cache_relpath(samples[i]) for i in idxs], (H, W), left, right, disp,
+                             self.read_threads)
+            return {"kind": 1, "index": torch.arange(n), "left": left, "right": right, "disparity": disp,
+                    "cache_file": [""] * n}
+
+        with ThreadPoolExecutor(1) as ex:
+            it = iter(self.loader.batch_sampler)
+            nxt = next(it, None)
+            fut = ex.submit(read, 0, nxt) if nxt is not None else None
+            k = 0
+            while fut is not None:
+                g = fut.result()
+                nxt = next(it, None)
+                fut = None
+                if nxt is not None:
+                    if self._h2d_done[k ^ 1] is not None:
+                        self._h2d_done[k ^ 1].synchronize()
+                    fut = ex.submit(read, k ^ 1, nxt)
+                self._slot = k
+                yield [g]
+                k ^= 1
+
     def __iter__(self):
         if self._stream is None:
             self._stream = torch.cuda.Stream(self.device)
         consumer = torch.cuda.current_stream(self.device)
         pending = None
-        for groups in self.loader:
+        for groups in (self._native_groups() if self.native else self.loader):
             self._stream.wait_stream(consumer)  # reuse of freed buffers is ordered after their last use
             with torch.cuda.stream(self._stream):
                 batch = self._prepare(groups)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
+            if self.native:
+                self._h2d_done[self._slot] = ev  # the pinned set may be refilled once its copies are done
             if pending is not None:
                 yield self._hand_over(*pending, consumer)
             pending = (batch, ev)

@@ -138,3 +138,37 @@ def test_collate_groups_by_kind_and_size(tmp_path):
     assert groups[0]["index"].tolist() == [0, 2, 3] and groups[1]["index"].tolist() == [1]
     assert groups[0]["left"].shape == (3, 45, 61, 3) and groups[0]["left"].dtype == torch.uint8
     assert groups[1]["disparity"].dtype == torch.int16
+
+
+def test_native_cache_reader_matches_numpy_load(tmp_path):
+    """sd_read_cache_batch (host C++, no GPU) returns exactly what the reference's load_cached_sample reads with
+    np.load from files in its format (save_cached_sample = reference dataset.py:108-128), and rejects what the
+    reference would: a missing entry, another image size, a non-savez (compressed) file."""
+    rng = np.random.default_rng(3)
+    H, W, n = 24, 32, 5
+    paths, ref = [], []
+    for i in range(n):
+        left = rng.uniform(0, 1, (3, H, W)).astype(np.float32)
+        right = rng.uniform(0, 1, (3, H, W)).astype(np.float32)
+        tgt = rng.uniform(0, 90, (1, H, W)).astype(np.float32)
+        f = tmp_path / f"s{i // 3}" / f"{i:06d}.npz"
+        D.save_cached_sample(f, left, right, tgt)
+        with np.load(f) as c:
+            ref.append((c["left"], c["right"], c["disparity"]))
+        paths.append(f)
+    lt = torch.empty(n, H, W, 3, dtype=torch.uint8)
+    rt = torch.empty_like(lt)
+    dt = torch.empty(n, H, W, dtype=torch.int16)
+    D.read_cache_batch(paths, (H, W), lt, rt, dt, threads=3)
+    for i, (l_, r_, d_) in enumerate(ref):
+        assert np.array_equal(lt[i].numpy(), l_) and np.array_equal(rt[i].numpy(), r_)
+        assert np.array_equal(dt[i].numpy().view(np.float16), d_)
+    with pytest.raises(FileNotFoundError, match="not found"):
+        D.read_cache_batch(paths[:2] + [tmp_path / "missing.npz"], (H, W), lt[:3], rt[:3], dt[:3])
+    with pytest.raises(ValueError, match="shape-mismatched"):
+        D.read_cache_batch(paths[:1], (H, W + 8), torch.empty(1, H, W + 8, 3, dtype=torch.uint8),
+                           torch.empty(1, H, W + 8, 3, dtype=torch.uint8), torch.empty(1, H, W + 8, dtype=torch.int16))
+    comp = tmp_path / "compressed.npz"
+    np.savez_compressed(comp, left=ref[0][0], right=ref[0][1], disparity=ref[0][2])
+    with pytest.raises(ValueError, match="compressed"):
+        D.read_cache_batch([comp], (H, W), lt[:1], rt[:1], dt[:1])

@@ -197,3 +197,29 @@ def test_run_epoch_on_device_loader(tmp_path):
     metrics, step = run_epoch(model, D.DeviceLoader(ds, batch_size=2, shuffle=True, device=DEV), DEV, optimizer=opt)
     assert step == 2 and set(metrics) == {"loss", "nll", "mae", "rmse", "sigma"}
     assert all(np.isfinite(v) for v in metrics.values())
+
+
+def test_device_loader_native_reader_matches_dataloader_path(tmp_path):
+    """DeviceLoader(native=True) (in-process C++ cache reader, two pinned buffer sets) yields the same batches, in
+    the same shuffled order, as the DataLoader worker path over the same cache; it is the default for a
+    require_cache dataset without augmentation."""
+    from stereo_depth_estimation_amd import dataset as D
+
+    write_stereo_tree(tmp_path / "data", scenes=2, frames=5, hw=(45, 61), seed=7)
+    samples = D.discover_samples(tmp_path / "data")
+    ds = D.FoundationStereoDataset(samples, image_size=(24, 32), cache_root=tmp_path / "cache")
+    for _ in D.DeviceLoader(ds, batch_size=4, device=DEV):  # first pass writes the cache
+        pass
+    torch.cuda.synchronize()
+    dsc = D.FoundationStereoDataset(samples, image_size=(24, 32), cache_root=tmp_path / "cache", require_cache=True)
+    assert D.DeviceLoader(dsc, batch_size=3, device=DEV).native
+    runs = {}
+    for native in (True, False):
+        ld = D.DeviceLoader(dsc, batch_size=3, shuffle=True, device=DEV, generator=torch.Generator().manual_seed(5),
+                            native=native, num_workers=0 if native else 2)
+        assert ld.native is native
+        runs[native] = [{k: v.cpu() for k, v in b.items()} for b in ld]
+    assert [b["input"].shape[0] for b in runs[True]] == [3, 3, 3, 1]
+    for a, b in zip(runs[True], runs[False]):
+        for k in ("input", "target", "valid_mask"):
+            assert torch.equal(a[k], b[k]), k
