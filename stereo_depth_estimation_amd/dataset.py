@@ -405,6 +405,9 @@ class DeviceLoader:
                     "cache_file": [""] * n}
 
         with ThreadPoolExecutor(1) as ex:
+            # a DataLoader iterator draws its workers' base seed from the generator (or the global RNG) before the
+            # sampler's permutation: the same draw keeps the shuffle order, and the RNG stream after it, identical
+            torch.empty((), dtype=torch.int64).random_(generator=self.loader.generator)
             it = iter(self.loader.batch_sampler)
             nxt = next(it, None)
             fut = ex.submit(read, 0, nxt) if nxt is not None else None
