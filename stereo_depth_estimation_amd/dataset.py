@@ -315,13 +315,14 @@ class DeviceLoader:
                  generator: torch.Generator | None = None, sampler=None, native: bool | None = None,
                  read_threads: int = 16):
         """native: read batches with the in-process native cache reader (``read_cache_batch``) instead of DataLoader
-        worker processes. Default (None): on for datasets served entirely from the cache (require_cache) without
-        augmentation, the case it covers; same batch order (the DataLoader's own batch sampler) and bytes."""
+        worker processes. Default (None): on for datasets served entirely from the cache (require_cache). Same batch
+        order (the DataLoader's own batch sampler) and bytes; augmentation factors are drawn in the main process in
+        the order of a num_workers=0 DataLoader (worker processes draw them from per-worker RNG streams instead)."""
         self.dataset = dataset
         if native is None:
-            native = dataset.cache_root is not None and dataset.require_cache and not dataset.augment
-        if native and (dataset.cache_root is None or dataset.augment):
-            raise ValueError("DeviceLoader(native=True) needs a cache_root and augment=False")
+            native = dataset.cache_root is not None and dataset.require_cache
+        if native and dataset.cache_root is None:
+            raise ValueError("DeviceLoader(native=True) reads the sample cache: the dataset needs a cache_root")
         self.native, self.read_threads = native, read_threads
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -420,6 +421,13 @@ class DeviceLoader:
                     if self._h2d_done[k ^ 1] is not None:
                         self._h2d_done[k ^ 1].synchronize()
                     fut = ex.submit(read, k ^ 1, nxt)
+                if self.dataset.augment:
+                    # drawn here, as batch k is handed over, so the main-process RNG sees the order of a
+                    # num_workers=0 DataLoader: factors of batch k (per item, in __getitem__'s calls), then the
+                    # noise seed _prepare draws for batch k, then batch k+1's factors
+                    ds = self.dataset
+                    g["aug"] = torch.from_numpy(np.stack([np.stack([ds.sample_augment_params(), ds.sample_augment_params()])
+                                                          for _ in range(len(g["index"]))]))
                 self._slot = k
                 yield [g]
                 k ^= 1

@@ -223,3 +223,16 @@ def test_device_loader_native_reader_matches_dataloader_path(tmp_path):
     for a, b in zip(runs[True], runs[False]):
         for k in ("input", "target", "valid_mask"):
             assert torch.equal(a[k], b[k]), k
+    # with augmentation: the factors and noise seeds come from the global RNG in a num_workers=0 DataLoader's order
+    dsa = D.FoundationStereoDataset(samples, image_size=(24, 32), cache_root=tmp_path / "cache", require_cache=True,
+                                    augment=True, brightness_jitter=0.2, hue_jitter=0.05, blur_prob=0.5,
+                                    blur_sigma_max=1.0, noise_std_max=0.02)
+    runs = {}
+    for native in (True, False):
+        torch.manual_seed(11)
+        ld = D.DeviceLoader(dsa, batch_size=4, shuffle=True, device=DEV, native=native, num_workers=0)
+        runs[native] = [{k: v.cpu() for k, v in b.items()} for _ in range(2) for b in ld]  # two epochs
+    assert len(runs[True]) == len(runs[False]) == 6
+    for a, b in zip(runs[True], runs[False]):
+        for k in ("input", "target", "valid_mask"):
+            assert torch.equal(a[k], b[k]), ("aug", k)
