@@ -135,6 +135,12 @@ def main():
             out[f"loader_cache_w{w}_pairs_s"] = round(loader_rate(cached, batch, w), 1)
             out[f"loader_png_aug_w{w}_pairs_s"] = round(loader_rate(png_aug, batch, w), 1)
             print(f"loaders w={w}: {out}", file=sys.stderr, flush=True)
+        cached_aug = D.FoundationStereoDataset(samples, image_size=(H, W), cache_root=cache, require_cache=True,
+                                               augment=True, brightness_jitter=0.2, contrast_jitter=0.2,
+                                               saturation_jitter=0.2, hue_jitter=0.05, gamma_jitter=0.1,
+                                               noise_std_max=0.02, blur_prob=0.3, blur_sigma_max=1.0)
+        out["loader_cache_aug_native_t16_pairs_s"] = round(loader_rate(cached_aug, batch, 0, native=True), 1)
+        out["train_cache_aug_native_t16_pairs_s"] = round(train_rate(cached_aug, batch, 0, native=True), 1)
         out["loader_cache_native_t16_pairs_s"] = round(loader_rate(cached, batch, 0, native=True), 1)
         out["train_cache_native_t16_pairs_s"] = round(train_rate(cached, batch, 0, native=True), 1)
         print(f"native: {out}", file=sys.stderr, flush=True)
