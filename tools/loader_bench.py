@@ -112,6 +112,7 @@ def main():
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 320
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else 64
     out = {"pairs": pairs, "hw": [H, W], "batch": batch}
+    quick = len(sys.argv) > 5 and sys.argv[5] == "quick"  # native training arm only (A/B runs)
     with tempfile.TemporaryDirectory(dir="/tmp") as tmp:
         root, cache = Path(tmp) / "data", Path(tmp) / "cache"
         t0 = time.perf_counter()
@@ -128,6 +129,10 @@ def main():
                                             contrast_jitter=0.2, saturation_jitter=0.2, hue_jitter=0.05,
                                             gamma_jitter=0.1, noise_std_max=0.02, blur_prob=0.3, blur_sigma_max=1.0)
         print(f"tree + cache written: {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+        if quick:
+            out["train_cache_native_t16_pairs_s"] = round(train_rate(cached, batch, 0, native=True, epochs=4), 1)
+            print(json.dumps(out), flush=True)
+            return
         out["host_enqueue_ms_per_step"], out["gpu_ms_per_step"] = (round(v, 2) for v in host_enqueue_ms(batch, H, W))
         out["host_dataloader_cache_w16_pairs_s"] = round(host_loader_rate(cached, batch, 16), 1)
         print(f"host: {out}", file=sys.stderr, flush=True)
