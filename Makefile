@@ -20,7 +20,7 @@ build/%.cpp.o: $(PKG)/csrc/%.cpp include/stereo_hip.h
 	$(CXX) -O3 -std=c++17 -fPIC -Wall -pthread -Iinclude -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $(OBJS) -lz
 
 clean:
 	rm -rf build $(LIB)

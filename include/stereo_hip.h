@@ -155,6 +155,12 @@ int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int
 int sd_read_cache_batch(const char* const* paths, int n, int H, int W, uint8_t* left, uint8_t* right,
                         uint16_t* disparity, int threads, char* err, int errlen);
 
+/* PNG frames of the un-cached source (reference dataset.py:23-30,184-212: PIL open + convert("RGB")): 8-bit RGB or
+ * RGBA, not interlaced. sd_png_size reads the IHDR; sd_read_png_batch decodes n frames of H x W with `threads` host
+ * threads into out [n][H][W][3]. Returns as sd_read_cache_batch (other PNG kinds: an error, for a PIL fallback). */
+int sd_png_size(const char* path, int* height, int* width);
+int sd_read_png_batch(const char* const* paths, int n, int H, int W, uint8_t* out, int threads, char* err, int errlen);
+
 /* ---- BatchNorm2d train/eval (model.py:37,40; native_batch_norm / _backward) ---- */
 int sd_bn_fwd_finalize(const float* stats, int rows, int C, double count, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,

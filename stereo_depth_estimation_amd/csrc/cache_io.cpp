@@ -175,3 +175,138 @@ extern "C" int sd_read_cache_batch(const char* const* paths, int n, int H, int W
     }
     return 0;
 }
+
+// ------------------------------------------------------------------ PNG frames (the un-cached source)
+// FoundationStereo frames and the RGB24 disparity codec images (reference dataset.py:23-30,184-212) are 8-bit RGB
+// or RGBA PNGs, not interlaced. Decoded here as PIL's Image.open(p).convert("RGB") returns them (alpha dropped);
+// other PNG kinds report an error and the caller falls back to PIL.
+#include <zlib.h>
+
+namespace {
+
+uint32_t be32(const unsigned char* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+bool png_header(const std::vector<unsigned char>& f, int& w, int& h, int& bpp, std::string& why) {
+    static const unsigned char sig[8] = {0x89, 'P', 'N', 'G', 0x0d, 0x0a, 0x1a, 0x0a};
+    if (f.size() < 33 || memcmp(f.data(), sig, 8) != 0 || memcmp(&f[12], "IHDR", 4) != 0) {
+        why = "not a PNG";
+        return false;
+    }
+    w = (int)be32(&f[16]);
+    h = (int)be32(&f[20]);
+    const int depth = f[24], color = f[25], interlace = f[28];
+    if (depth != 8 || (color != 2 && color != 6) || interlace != 0 || f[26] != 0 || f[27] != 0) {
+        why = "unsupported PNG kind (needs 8-bit RGB/RGBA, not interlaced)";
+        return false;
+    }
+    bpp = color == 2 ? 3 : 4;
+    return true;
+}
+
+unsigned char paeth(int a, int b, int c) {
+    const int p = a + b - c, pa = abs(p - a), pb = abs(p - b), pc = abs(p - c);
+    return (unsigned char)(pa <= pb && pa <= pc ? a : (pb <= pc ? b : c));
+}
+
+bool decode_png(const std::vector<unsigned char>& f, int H, int W, unsigned char* out, std::vector<unsigned char>& z,
+                std::vector<unsigned char>& raw, std::string& why) {
+    int w = 0, h = 0, bpp = 0;
+    if (!png_header(f, w, h, bpp, why)) return false;
+    if (w != W || h != H) {
+        why = "size " + std::to_string(h) + "x" + std::to_string(w) + " differs from the batch's";
+        return false;
+    }
+    z.clear();
+    for (size_t pos = 8; pos + 12 <= f.size();) {
+        const uint32_t len = be32(&f[pos]);
+        if (pos + 12 + (size_t)len > f.size()) break;
+        const unsigned char* type = &f[pos + 4];
+        if (memcmp(type, "IDAT", 4) == 0) z.insert(z.end(), f.begin() + pos + 8, f.begin() + pos + 8 + len);
+        if (memcmp(type, "IEND", 4) == 0) break;
+        pos += 12 + (size_t)len;
+    }
+    const size_t stride = (size_t)W * bpp;
+    raw.resize((size_t)H * (stride + 1));
+    uLongf got = (uLongf)raw.size();
+    if (uncompress(raw.data(), &got, z.data(), (uLong)z.size()) != Z_OK || got != raw.size()) {
+        why = "corrupt image data";
+        return false;
+    }
+    for (int y = 0; y < H; ++y) {  // unfilter in place (filter byte, then the row)
+        unsigned char* row = &raw[(size_t)y * (stride + 1) + 1];
+        const unsigned char* up = y ? &raw[(size_t)(y - 1) * (stride + 1) + 1] : nullptr;
+        const int ft = row[-1];
+        for (size_t x = 0; x < stride; ++x) {
+            const int a = x >= (size_t)bpp ? row[x - bpp] : 0, b = up ? up[x] : 0;
+            const int c = (up && x >= (size_t)bpp) ? up[x - bpp] : 0;
+            switch (ft) {
+                case 0: break;
+                case 1: row[x] = (unsigned char)(row[x] + a); break;
+                case 2: row[x] = (unsigned char)(row[x] + b); break;
+                case 3: row[x] = (unsigned char)(row[x] + ((a + b) >> 1)); break;
+                case 4: row[x] = (unsigned char)(row[x] + paeth(a, b, c)); break;
+                default: why = "bad filter type"; return false;
+            }
+        }
+        unsigned char* o = out + (size_t)y * W * 3;
+        if (bpp == 3) {
+            memcpy(o, row, stride);
+        } else {
+            for (int x = 0; x < W; ++x) {
+                o[3 * x] = row[4 * x];
+                o[3 * x + 1] = row[4 * x + 1];
+                o[3 * x + 2] = row[4 * x + 2];
+            }
+        }
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" int sd_png_size(const char* path, int* height, int* width) {
+    std::vector<unsigned char> f;
+    std::string why;
+    int bpp = 0;
+    if (!path || !height || !width || !read_file(path, f, why) || !png_header(f, *width, *height, bpp, why)) return -1;
+    return 0;
+}
+
+extern "C" int sd_read_png_batch(const char* const* paths, int n, int H, int W, uint8_t* out, int threads, char* err,
+                                 int errlen) {
+    if (!paths || n < 0 || H <= 0 || W <= 0 || !out) {
+        if (err && errlen > 0) snprintf(err, (size_t)errlen, "sd_read_png_batch: bad args");
+        return -1;
+    }
+    if (threads < 1) threads = 1;
+    if (threads > n) threads = n > 0 ? n : 1;
+    std::atomic<int> next{0}, first_bad{n};
+    std::mutex mu;
+    std::string bad_why;
+    auto work = [&]() {
+        std::vector<unsigned char> buf, z, raw;
+        std::string why;
+        for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) {
+            bool ok = paths[i] && read_file(paths[i], buf, why);
+            if (ok) ok = decode_png(buf, H, W, out + (size_t)i * H * W * 3, z, raw, why);
+            if (!ok) {
+                std::lock_guard<std::mutex> g(mu);
+                if (i < first_bad.load()) {
+                    first_bad.store(i);
+                    bad_why = why;
+                }
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    const int bad = first_bad.load();
+    if (bad < n) {
+        if (err && errlen > 0)
+            snprintf(err, (size_t)errlen, "%s: %s", paths[bad] ? paths[bad] : "(null)", bad_why.c_str());
+        return bad + 1;
+    }
+    return 0;
+}

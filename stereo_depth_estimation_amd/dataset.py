@@ -300,6 +300,29 @@ def read_cache_batch(paths, image_size: tuple[int, int], left: torch.Tensor, rig
         raise ValueError(f"Cache entry is invalid or shape-mismatched: {msg}")
 
 
+def read_png_batch(paths, size: tuple[int, int], out: torch.Tensor, threads: int = 16) -> bool:
+    """Native (``sd_read_png_batch``) decode of n PNG frames of one source size into a uint8 [n,H,W,3] host tensor,
+    as ``read_rgb_uint8`` (PIL ``convert("RGB")``) returns them. False when a file is not an 8-bit RGB/RGBA,
+    non-interlaced PNG of that size (the caller reads that batch with PIL); missing files raise."""
+    H, W = size
+    n = len(paths)
+    if tuple(out.shape) != (n, H, W, 3) or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise ValueError(f"read_png_batch: expected a contiguous uint8 tensor of {(n, H, W, 3)}")
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(str(p)) for p in paths])
+    err = ctypes.create_string_buffer(1024)
+    rc = L.load().sd_read_png_batch(ctypes.cast(arr, ctypes.c_void_p), n, H, W, out.data_ptr(), threads, err, len(err))
+    if rc > 0 and not Path(paths[rc - 1]).exists():
+        raise FileNotFoundError(err.value.decode(errors="replace"))
+    return rc == 0
+
+
+def png_size(path) -> tuple[int, int] | None:
+    """(H, W) from a PNG's IHDR, None if it is not a PNG."""
+    h, w = ctypes.c_int(0), ctypes.c_int(0)
+    rc = L.load().sd_png_size(os.fsencode(str(path)), ctypes.addressof(h), ctypes.addressof(w))
+    return (h.value, w.value) if rc == 0 else None
+
+
 class DeviceLoader:
     """Iterates device batch dicts ``{"input","target","valid_mask"}`` for ``run_epoch``.
 
@@ -315,14 +338,16 @@ class DeviceLoader:
                  generator: torch.Generator | None = None, sampler=None, native: bool | None = None,
                  read_threads: int = 16):
         """native: read batches with the in-process native cache reader (``read_cache_batch``) instead of DataLoader
-        worker processes. Default (None): on for datasets served entirely from the cache (require_cache). Same batch
+        worker processes; without a cache_root (native=True only), PNG frames decoded by ``read_png_batch``. Default
+        (None): on for datasets served entirely from the cache (require_cache). Same batch
         order (the DataLoader's own batch sampler) and bytes; augmentation factors are drawn in the main process in
         the order of a num_workers=0 DataLoader (worker processes draw them from per-worker RNG streams instead)."""
         self.dataset = dataset
         if native is None:
             native = dataset.cache_root is not None and dataset.require_cache
-        if native and dataset.cache_root is None:
-            raise ValueError("DeviceLoader(native=True) reads the sample cache: the dataset needs a cache_root")
+        if native and dataset.cache_root is not None and not dataset.require_cache:
+            raise ValueError("DeviceLoader(native=True) serves a cache_root dataset only with require_cache "
+                             "(the worker path writes cache misses)")
         self.native, self.read_threads = native, read_threads
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -394,10 +419,28 @@ class DeviceLoader:
                     torch.empty(bmax, H, W, 3, dtype=torch.uint8).pin_memory(),
                     torch.empty(bmax, H, W, dtype=torch.int16).pin_memory())
 
-        bufs = [alloc(), alloc()]
+        bufs = [alloc(), alloc()] if root is not None else [None, None]
         self._h2d_done = [None, None]
 
+        def read_png(idxs):  # frames of the un-cached source (pinned by torch's caching host allocator)
+            n = len(idxs)
+            sm = [samples[i] for i in idxs]
+            hw = png_size(sm[0].left_rgb_path)
+            outs = []
+            for attr in ("left_rgb_path", "right_rgb_path", "disparity_path"):
+                paths = [getattr(x, attr) for x in sm]
+                t = torch.empty(n, *(hw or (1, 1)), 3, dtype=torch.uint8, pin_memory=True)
+                if hw is None or not read_png_batch(paths, hw, t, self.read_threads):
+                    t = torch.from_numpy(np.stack([read_rgb_uint8(p) for p in paths])).pin_memory()
+                outs.append(t)
+            if not (outs[0].shape == outs[1].shape == outs[2].shape):
+                raise ValueError(f"left/right/disparity sizes differ in the batch of {sm[0].disparity_path}")
+            return {"kind": 0, "index": torch.arange(n), "left": outs[0], "right": outs[1], "disparity": outs[2],
+                    "cache_file": [""] * n}
+
         def read(k, idxs):
+            if root is None:
+                return read_png(idxs)
             n = len(idxs)
             left, right, disp = (t[:n] for t in bufs[k])
             read_cache_batch([root / sample_cache_relpath(samples[i]) for i in idxs], (H, W), left, right, disp,

@@ -172,3 +172,67 @@ def test_native_cache_reader_matches_numpy_load(tmp_path):
     np.savez_compressed(comp, left=ref[0][0], right=ref[0][1], disparity=ref[0][2])
     with pytest.raises(ValueError, match="compressed"):
         D.read_cache_batch([comp], (H, W), lt[:1], rt[:1], dt[:1])
+
+
+def _png_with_filters(path, img):
+    """An 8-bit RGB/RGBA PNG whose row y uses filter type y % 5 (None, Sub, Up, Average, Paeth)."""
+    import struct
+    import zlib
+
+    h, w, c = img.shape
+    bpp, rows, prev = c, [], np.zeros(w * c, np.int32)
+    for y in range(h):
+        cur = img[y].reshape(-1).astype(np.int32)
+        a = np.concatenate([np.zeros(bpp, np.int32), cur[:-bpp]])
+        cc = np.concatenate([np.zeros(bpp, np.int32), prev[:-bpp]])
+        ft = y % 5
+        if ft == 0:
+            pred = np.zeros_like(cur)
+        elif ft == 1:
+            pred = a
+        elif ft == 2:
+            pred = prev
+        elif ft == 3:
+            pred = (a + prev) // 2
+        else:
+            p = a + prev - cc
+            pa, pb, pc = np.abs(p - a), np.abs(p - prev), np.abs(p - cc)
+            pred = np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, prev, cc))
+        rows.append(bytes([ft]) + ((cur - pred) % 256).astype(np.uint8).tobytes())
+        prev = cur
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+    ihdr = struct.pack(">IIBBBBB", w, h, 8, 2 if c == 3 else 6, 0, 0, 0)
+    path.write_bytes(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(b"".join(rows)))
+                     + chunk(b"IEND", b""))
+
+
+def test_native_png_reader_matches_pil(tmp_path):
+    """sd_read_png_batch decodes what read_rgb_uint8 (PIL convert("RGB"), reference dataset.py:184-212) returns:
+    RGB and RGBA frames, every PNG row filter, PIL-written files; other kinds report False (PIL fallback)."""
+    from PIL import Image
+
+    rng = np.random.default_rng(5)
+    H, W = 19, 23
+    paths = []
+    for i in range(6):
+        img = rng.integers(0, 256, (H, W, 3 if i % 2 == 0 else 4), dtype=np.uint8)
+        p = tmp_path / f"f{i}.png"
+        if i < 4:
+            _png_with_filters(p, img)
+        else:
+            Image.fromarray(img).save(p)
+        paths.append(p)
+    assert D.png_size(paths[0]) == (H, W)
+    out = torch.empty(len(paths), H, W, 3, dtype=torch.uint8)
+    assert D.read_png_batch(paths, (H, W), out, threads=3)
+    for i, p in enumerate(paths):
+        assert np.array_equal(out[i].numpy(), D.read_rgb_uint8(p)), i
+    gray = tmp_path / "gray.png"
+    Image.fromarray(rng.integers(0, 256, (H, W), dtype=np.uint8)).save(gray)
+    assert not D.read_png_batch([gray], (H, W), out[:1])
+    assert not D.read_png_batch(paths[:1], (H, W + 1), torch.empty(1, H, W + 1, 3, dtype=torch.uint8))
+    with pytest.raises(FileNotFoundError):
+        D.read_png_batch([tmp_path / "missing.png"], (H, W), out[:1])

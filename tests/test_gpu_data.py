@@ -236,3 +236,25 @@ def test_device_loader_native_reader_matches_dataloader_path(tmp_path):
     for a, b in zip(runs[True], runs[False]):
         for k in ("input", "target", "valid_mask"):
             assert torch.equal(a[k], b[k]), ("aug", k)
+
+
+def test_device_loader_native_png_matches_dataloader_path(tmp_path):
+    """DeviceLoader(native=True) on an un-cached PNG dataset (frames decoded by the C++ reader, then the same
+    sd_stereo_preprocess) equals the DataLoader path, plain and with augmentation (RNG in a num_workers=0 order)."""
+    from stereo_depth_estimation_amd import dataset as D
+
+    write_stereo_tree(tmp_path / "data", scenes=2, frames=5, hw=(45, 61), seed=9)
+    samples = D.discover_samples(tmp_path / "data")
+    for aug in (False, True):
+        ds = D.FoundationStereoDataset(samples, image_size=(24, 32), augment=aug, brightness_jitter=0.2,
+                                       hue_jitter=0.05, blur_prob=0.5, blur_sigma_max=1.0, noise_std_max=0.02)
+        assert not D.DeviceLoader(ds, batch_size=3, device=DEV).native  # opt-in for PNG sources
+        runs = {}
+        for native in (True, False):
+            torch.manual_seed(13)
+            ld = D.DeviceLoader(ds, batch_size=3, shuffle=True, device=DEV, native=native, num_workers=0)
+            runs[native] = [{k: v.cpu() for k, v in b.items()} for b in ld]
+        assert [b["input"].shape[0] for b in runs[True]] == [3, 3, 3, 1]
+        for a, b in zip(runs[True], runs[False]):
+            for k in ("input", "target", "valid_mask"):
+                assert torch.equal(a[k], b[k]), (aug, k)

@@ -146,6 +146,8 @@ def main():
                                                noise_std_max=0.02, blur_prob=0.3, blur_sigma_max=1.0)
         out["loader_cache_aug_native_t16_pairs_s"] = round(loader_rate(cached_aug, batch, 0, native=True), 1)
         out["train_cache_aug_native_t16_pairs_s"] = round(train_rate(cached_aug, batch, 0, native=True), 1)
+        out["loader_png_aug_native_t16_pairs_s"] = round(loader_rate(png_aug, batch, 0, native=True), 1)
+        out["train_png_aug_native_t16_pairs_s"] = round(train_rate(png_aug, batch, 0, native=True), 1)
         out["loader_cache_native_t16_pairs_s"] = round(loader_rate(cached, batch, 0, native=True), 1)
         out["train_cache_native_t16_pairs_s"] = round(train_rate(cached, batch, 0, native=True), 1)
         print(f"native: {out}", file=sys.stderr, flush=True)
