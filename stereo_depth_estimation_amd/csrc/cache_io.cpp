@@ -1,4 +1,5 @@
-// Native reader for the reference's sample cache (reference dataset.py:86-105 load_cached_sample, cache.py:50-112):
+// Native host readers for the data path: the reference's sample cache and its PNG frames.
+// Sample cache (reference dataset.py:86-105 load_cached_sample, cache.py:50-112):
 // one np.savez file per pair, an uncompressed zip of left.npy / right.npy (uint8 HWC) and disparity.npy (f16 HW).
 // A batch of files is read by a pool of threads straight into the caller's (pinned) host buffers, so the data path
 // needs no worker processes, no pickling and no second pinning copy (tools/loader_bench.py: the torch DataLoader
@@ -6,10 +7,12 @@
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -180,7 +183,6 @@ extern "C" int sd_read_cache_batch(const char* const* paths, int n, int H, int W
 // FoundationStereo frames and the RGB24 disparity codec images (reference dataset.py:23-30,184-212) are 8-bit RGB
 // or RGBA PNGs, not interlaced. Decoded here as PIL's Image.open(p).convert("RGB") returns them (alpha dropped);
 // other PNG kinds report an error and the caller falls back to PIL.
-#include <zlib.h>
 
 namespace {
 
