@@ -20,9 +20,11 @@ TFLOP/s dense bf16 (MI355X_MICROARCH.md). `traffic` = that kernel's HBM bytes pe
 the committed rocprofv3 PMC summary of this same command (profiles/pmc_traffic.json, made by
 tools/pmc_traffic.py: 1024*(2*FETCH_SIZE + WRITE_SIZE), the guide's gfx950 corrections).
 `cpu_baseline`: the oracle's PyTorch-CPU fp32 restatement of the reference train step (B=2,
-320x240), timed on this host (rank 0, N=1). `epe_vs_fp32`: mean |disparity(bf16) -
-disparity(fp32)| of this framework's two precisions on one batch with the trained weights
-(the fp32 path is pinned to the reference within 1e-3 per pixel by tests/test_gpu_model.py).
+320x240), timed on this host (rank 0, N=1). `epe` (N=1): after --epe-steps synthetic training
+steps, the validation EPE (the reference's `mae`) of the bf16 path, the fp32 path (pinned to the
+reference within 1e-3 per pixel by the tests) and their difference.
+`comm` (N>1): process-group backend and world size, bucket sizes, and the all-reduce time per
+step that backward did not hide.
 """
 
 from __future__ import annotations
@@ -58,6 +60,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-infer", action="store_true", help="skip the 960x720 fp8/bf16/fp32 inference lines")
     ap.add_argument("--sync-bn", action="store_true", help="N > 1: global-batch BatchNorm statistics (SyncBatchNorm)")
+    ap.add_argument("--epe-steps", type=int, default=2000,
+                    help="N=1: synthetic training steps before the EPE comparison (0 skips it)")
     return ap.parse_args()
 
 
@@ -195,33 +199,70 @@ class GemmTimer:
                  "tflops": fl / (ms * 1e-3) / 1e12, "ms_per_step": ms / steps} for ms, k, n, fl in rows]
 
 
+def lib_sha256() -> str:
+    import hashlib
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stereo_depth_estimation_amd", "libstereo_hip.so")
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
+    """(HBM bytes per launch of `kernel`, source note) from the committed PMC summary. The bytes are None unless the
+    summary was collected from this very library build (its lib_sha256 equals the loaded .so's)."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            k = json.load(f)["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
-        return None
-    return None if k is None else k.get("hbm_bytes_per_launch")
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC summary"
+    sha = lib_sha256()
+    if d.get("lib_sha256") != sha:
+        return None, f"profiles/pmc_traffic.json is from another build ({str(d.get('lib_sha256'))[:12]} != {sha[:12]})"
+    k = d.get("kernels", {}).get(kernel)
+    if k is None:
+        return None, "kernel not in profiles/pmc_traffic.json"
+    return k.get("hbm_bytes_per_launch"), f"profiles/pmc_traffic.json (same build, {sha[:12]})"
 
 
-def epe_vs_fp32(torch, model, batch, pairs: int = 8):
-    """EPE between the bf16 and fp32 HIP forwards (eval mode, same weights and BN statistics)."""
+def epe_block(torch, model, opt, dev, steps: int):
+    """North star "disparity EPE within 1e-3 of reference" (EPE = the reference's `mae`, the mean |pred - target| over
+    valid pixels, train.py:350,406). The bench model is first trained on synthetic pairs (bf16, lr 1e-3, the
+    reference's AdamW) until its disparity tracks the targets; then the validation epoch (eval BN, train.py:301)
+    runs on held-out synthetic pairs with the same weights in bf16 and in fp32 (the fp32 path is held to the
+    reference's CPU path within 1e-3 per pixel; tests/test_gpu_configs.py also checks both EPEs against the CPU
+    oracle on a trained checkpoint)."""
+    from stereo_depth_estimation_amd.data import synthetic_batch
     from stereo_depth_estimation_amd.model import StereoUNet
+    from stereo_depth_estimation_amd.train import run_epoch, train_step
 
-    ref = StereoUNet(precision="fp32").to(batch["input"].device)
-    ref.load_state_dict(model.state_dict())
-    model.eval()
-    ref.eval()
-    x = batch["input"][:pairs]
-    with torch.no_grad():
-        d16 = model(x)
-        d32 = ref(x)
+    train = [synthetic_batch(64, 240, 320, seed=50_000 + i, device=dev) for i in range(16)]
+    t0 = time.perf_counter()
     model.train()
-    epe = float((d16 - d32).abs().mean())
-    return {"value": round(epe, 5), "unit": "px", "pairs": int(x.shape[0]),
-            "mean_disparity_fp32": round(float(d32.mean()), 4), "max_abs": round(float((d16 - d32).abs().max()), 5)}
+    for i in range(steps):
+        b = train[i % len(train)]
+        train_step(model, opt, b["input"], b["target"], b["valid_mask"])
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t0
+    val = [synthetic_batch(64, 240, 320, seed=90_000 + i, device=dev) for i in range(2)]
+    m16, _ = run_epoch(model, val, dev, optimizer=None)
+    ref = StereoUNet(precision="fp32").to(dev)
+    ref.load_state_dict(model.state_dict())
+    m32, _ = run_epoch(ref, val, dev, optimizer=None)
+    ref.eval()
+    model.eval()
+    with torch.no_grad():
+        d16, d32 = model(val[0]["input"]), ref(val[0]["input"])
+    vmask = val[0]["valid_mask"]
+    res = {"train_steps": steps, "train_s": round(t_train, 2), "eval_pairs": 128,
+           "epe_bf16": round(m16["mae"], 6), "epe_fp32": round(m32["mae"], 6),
+           "delta": round(abs(m16["mae"] - m32["mae"]), 6), "target": 1e-3,
+           "met": abs(m16["mae"] - m32["mae"]) < 1e-3,
+           "mean_disparity": round(float(d32[vmask].mean()), 3), "mean_target": round(float(val[0]["target"][vmask].mean()), 3),
+           "per_pixel_bf16_vs_fp32": {"mean": round(float((d16 - d32).abs().mean()), 6),
+                                      "max": round(float((d16 - d32).abs().max()), 6)}}
+    model.train()
+    return res
 
 
 def infer_fp8(torch, model, dev, H=720, W=960, iters=20):
@@ -361,6 +402,8 @@ def main():
     if not args.no_roofline:
         timer = GemmTimer(torch, L, model._engine)
         L.set_call_hook(timer)
+        if ddp is not None:
+            ddp._reducer().wait_events = []
         for i in range(args.steps):
             step(i)
         torch.cuda.synchronize()
@@ -398,20 +441,37 @@ def main():
     }
     if share:
         result["rehearsal"] = f"gloo, {world} ranks sharing cuda:0 (SD_BENCH_SHARE_DEVICE=1): not a scaling number"
+    if world > 1:
+        ar = ddp._reducer()
+        comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "buckets": len(ar.buckets),
+                "bucket_mb": [round((b - a) * 4 / 2**20, 2) for _, a, b in ar.buckets]}
+        if ar.wait_events:
+            torch.cuda.synchronize()
+            exposed = sum(a.elapsed_time(b) for a, b in ar.wait_events) / args.steps
+            t = torch.tensor([exposed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            comm["allreduce_exposed_ms_per_step"] = round(float(t.item()), 4)
+            comm["exposed_region"] = "HIP events around the bucket waits before AdamW, max over ranks (second region)"
+        result["comm"] = comm
     peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
     step_tflops = TRAIN_GFLOP_PER_PAIR * 1e9 * B * (H * W) / (240 * 320) / (dt / args.steps) / 1e12
     result["step_conv_tflops"] = round(step_tflops, 2)
     if timer is not None:
         kern = timer.summary(args.steps)
         top = kern[0]
+        traffic, tsrc = pmc_traffic(top["kernel"])
+        # arithmetic intensity against the ridge (peak FLOP/s / 8 TB/s); the layer map puts this family above it
+        ai = top["flops_per_launch"] / traffic if traffic else None
         result["roofline"] = {
-            "bound": "mfma",
+            "bound": "mfma" if ai is None or ai >= peak * 1e12 / 8e12 else "hbm",
             "kernel": top["kernel"],
             "achieved": round(top["tflops"], 2),
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(top["tflops"] / peak, 4),
-            "traffic": pmc_traffic(top["kernel"]),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "flop_per_byte": round(ai, 1) if ai else None,
             "avg_launch_us": round(top["avg_us"], 2),
             "flops_per_launch": top["flops_per_launch"],
             "launches_per_step": top["launches_per_step"],
@@ -419,8 +479,9 @@ def main():
         }
         result["gemm_kernels"] = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()} for r in kern]
         result["encoder_conv_roofline"] = timer.encoder_roofline(args.steps, peak)
-    if rank == 0:
-        result["epe_vs_fp32"] = epe_vs_fp32(torch, model, ring[0])
+    if world == 1 and args.epe_steps > 0:
+        log(f"EPE: {args.epe_steps} synthetic training steps, then bf16 / fp32 / oracle validation ...")
+        result["epe"] = epe_block(torch, model, opt, dev, args.epe_steps)
     if rank == 0 and world == 1 and not args.no_infer:
         log("fp8 inference (config 5) ...")
         result["infer_960x720"] = infer_fp8(torch, model, dev)

@@ -178,14 +178,15 @@ int sd_bn_bwd_finalize(const float* partials, int rows, int C, double count, con
                        const float* invstd, int batch_stats, float* dgamma, float* dbeta, float* coef, sd_stream s);
 /* SyncBatchNorm (SURVEY §8e "--sync-bn"; torch.nn.SyncBatchNorm semantics, replacing the per-rank reductions of
  * model.py:37,40 under DDP). Each rank reduces its float2 partial rows (the producer's STATS rows, or the
- * BatchNorm-backward partials) to fp64 sums[C][2]; the host all-reduces them (SUM) across ranks; the finalizes
- * below then use the global sums and the global pixel count. The backward writes dgamma/dbeta from local_sums
+ * BatchNorm-backward partials) to fp64 sums[2C + 1]: per channel (sum, sumsq), then this rank's pixel count; the
+ * host all-reduces the whole vector (SUM) across ranks, so the count that arrives is the global one whatever each
+ * rank's batch size; the finalizes below read it from sums[2C]. The backward writes dgamma/dbeta from local_sums
  * (the gradient all-reduce adds the ranks' shares) and coef from global_sums. */
-int sd_bn_rows_sum64(const float* rows, int nrows, int C, double* sums, sd_stream s);
-int sd_bn_fwd_finalize64(const double* sums, int C, double count, const float* gamma, const float* beta,
+int sd_bn_rows_sum64(const float* rows, int nrows, int C, double pixels, double* sums, sd_stream s);
+int sd_bn_fwd_finalize64(const double* sums, int C, const float* gamma, const float* beta,
                          float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,
                          float eps, float* mean, float* invstd, float* scale, float* shift, sd_stream s);
-int sd_bn_bwd_finalize64(const double* local_sums, const double* global_sums, int C, double count, const float* gamma,
+int sd_bn_bwd_finalize64(const double* local_sums, const double* global_sums, int C, const float* gamma,
                          const float* invstd, int batch_stats, float* dgamma, float* dbeta, float* coef, sd_stream s);
 /* dy = coef0 * (dz - coef1 - xhat*coef2) */
 int sd_bn_bwd_apply(int dtype, const void* da, const void* y, const float* scale, const float* shift,

@@ -117,9 +117,9 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_read_cache_batch": (_i, [_p, _i, _i, _i, _p, _p, _p, _i, ctypes.c_char_p, _i]),
     "sd_png_size": (_i, [ctypes.c_char_p, _p, _p]),
     "sd_read_png_batch": (_i, [_p, _i, _i, _i, _p, _i, ctypes.c_char_p, _i]),
-    "sd_bn_rows_sum64": (_i, [_p, _i, _i, _p, _p]),
-    "sd_bn_fwd_finalize64": (_i, [_p, _i, _d, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
-    "sd_bn_bwd_finalize64": (_i, [_p, _p, _i, _d, _p, _p, _i, _p, _p, _p, _p]),
+    "sd_bn_rows_sum64": (_i, [_p, _i, _i, _d, _p, _p]),
+    "sd_bn_fwd_finalize64": (_i, [_p, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
+    "sd_bn_bwd_finalize64": (_i, [_p, _p, _i, _p, _p, _i, _p, _p, _p, _p]),
     "sd_bn_bwd_apply": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _p]),
     "sd_pool_bwd_add": (_i, [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sd_pool_bwd_rows": (_i, [_i, _i, _i, _i]),

@@ -78,7 +78,7 @@ class TrainConfig:  # reference train.py:38-58, plus the HIP path's options at t
     blur_sigma_max: float
     blur_kernel_size: int
     resume: str | None = None
-    precision: str = "bf16"
+    precision: str = "fp32"
     sync_bn: bool = False
 
 
@@ -116,7 +116,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--blur-sigma-max", type=float, default=0.0)
     p.add_argument("--blur-kernel-size", type=int, default=5)
     p.add_argument("--resume", type=str, default=None, help="Checkpoint (last.pt) to continue from.")
-    p.add_argument("--precision", type=str, default="bf16", choices=("bf16", "fp32"))
+    p.add_argument("--precision", type=str, default="fp32", choices=("bf16", "fp32"),
+                   help="fp32: the reference's arithmetic (default); bf16: opt-in fast path (bf16 activations, fp32 accumulation)")
     p.add_argument("--sync-bn", action="store_true",
                    help="multi-GPU: BatchNorm statistics over the global batch (SyncBatchNorm) instead of per rank")
     return p
@@ -237,7 +238,7 @@ def main(argv=None) -> dict:
     if world > 1:
         import torch.distributed as dist
 
-        from .ddp import DataParallel
+        from .ddp import DataParallel, ShardSampler
 
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if not dist.is_initialized():
@@ -268,8 +269,8 @@ def main(argv=None) -> dict:
         from torch.utils.data.distributed import DistributedSampler
 
         sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
-        if val_ds is not None:
-            val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False)
+        if val_ds is not None:  # exact shards: no padded duplicates in the summed val metrics (best.pt selection)
+            val_sampler = ShardSampler(len(val_ds), world, rank)
     persistent = args.num_workers > 0
     loader_gen = None
     if persistent:

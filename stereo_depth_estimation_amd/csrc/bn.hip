@@ -69,8 +69,10 @@ __global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restric
 
 // SyncBatchNorm: the float2 partial rows of one rank -> fp64 per-channel sums[2c], sums[2c+1] (the same fixed-order
 // reduction the finalizes run), which the host all-reduces across ranks before the *_finalize64 kernels
-__global__ __launch_bounds__(256) void k_rows_sum64(const float2* __restrict__ rows_, int rows, int C, double* sums) {
+__global__ __launch_bounds__(256) void k_rows_sum64(const float2* __restrict__ rows_, int rows, int C, double pixels,
+                                                    double* sums) {
     const int c = blockIdx.x;
+    if (c == 0 && threadIdx.x == 0) sums[2 * C] = pixels;  // summed with the channel sums by the all-reduce
     double s = 0.0, ss = 0.0;
     for (int r = threadIdx.x; r < rows; r += 256) {
         const float2 v = rows_[(size_t)r * C + c];
@@ -84,12 +86,13 @@ __global__ __launch_bounds__(256) void k_rows_sum64(const float2* __restrict__ r
     }
 }
 
-__global__ __launch_bounds__(256) void k_bn_fwd_finalize64(const double* __restrict__ sums, int C, double count,
+__global__ __launch_bounds__(256) void k_bn_fwd_finalize64(const double* __restrict__ sums, int C,
                                                            const float* gamma, const float* beta, float* running_mean,
                                                            float* running_var, int64_t* nbt, float momentum, float eps,
                                                            float* mean_o, float* invstd_o, float* scale_o,
                                                            float* shift_o) {
     const int c = blockIdx.x * 256 + threadIdx.x;
+    const double count = sums[2 * C];  // global pixel count
     if (c < C)
         bn_fwd_emit(c, sums[2 * c], sums[2 * c + 1], count, gamma, beta, running_mean, running_var, nbt, momentum, eps,
                     mean_o, invstd_o, scale_o, shift_o);
@@ -207,10 +210,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restric
 }
 
 __global__ __launch_bounds__(256) void k_bn_bwd_finalize64(const double* __restrict__ local,
-                                                           const double* __restrict__ global, int C, double count,
+                                                           const double* __restrict__ global, int C,
                                                            const float* gamma, const float* invstd, int batch_stats,
                                                            float* dgamma, float* dbeta, float* coef) {
     const int c = blockIdx.x * 256 + threadIdx.x;
+    const double count = global[2 * C];  // global pixel count
     if (c < C)
         bn_bwd_emit(c, local[2 * c], local[2 * c + 1], global[2 * c], global[2 * c + 1], count, gamma, invstd,
                     batch_stats, dgamma, dbeta, coef);
@@ -386,31 +390,29 @@ extern "C" int sd_bn_fwd_finalize(const float* stats, int rows, int C, double co
     return sd_check_launch("sd_bn_fwd_finalize");
 }
 
-extern "C" int sd_bn_rows_sum64(const float* rows, int nrows, int C, double* sums, sd_stream s) {
-    SD_REQUIRE(rows && sums && nrows > 0 && C > 0, "sd_bn_rows_sum64: bad args");
-    hipLaunchKernelGGL(k_rows_sum64, dim3(C), dim3(256), 0, to_stream(s), (const float2*)rows, nrows, C, sums);
+extern "C" int sd_bn_rows_sum64(const float* rows, int nrows, int C, double pixels, double* sums, sd_stream s) {
+    SD_REQUIRE(rows && sums && nrows > 0 && C > 0 && pixels > 0, "sd_bn_rows_sum64: bad args");
+    hipLaunchKernelGGL(k_rows_sum64, dim3(C), dim3(256), 0, to_stream(s), (const float2*)rows, nrows, C, pixels, sums);
     return sd_check_launch("sd_bn_rows_sum64");
 }
 
-extern "C" int sd_bn_fwd_finalize64(const double* sums, int C, double count, const float* gamma, const float* beta,
+extern "C" int sd_bn_fwd_finalize64(const double* sums, int C, const float* gamma, const float* beta,
                                     float* running_mean, float* running_var, int64_t* num_batches_tracked,
                                     float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
                                     sd_stream s) {
-    SD_REQUIRE(sums && C > 0 && count > 0 && gamma && beta && mean && invstd && scale && shift,
-               "sd_bn_fwd_finalize64: bad args");
+    SD_REQUIRE(sums && C > 0 && gamma && beta && mean && invstd && scale && shift, "sd_bn_fwd_finalize64: bad args");
     SD_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "sd_bn_fwd_finalize64: running stats pair");
-    hipLaunchKernelGGL(k_bn_fwd_finalize64, dim3(cdiv(C, 256)), dim3(256), 0, to_stream(s), sums, C, count, gamma, beta,
+    hipLaunchKernelGGL(k_bn_fwd_finalize64, dim3(cdiv(C, 256)), dim3(256), 0, to_stream(s), sums, C, gamma, beta,
                        running_mean, running_var, num_batches_tracked, momentum, eps, mean, invstd, scale, shift);
     return sd_check_launch("sd_bn_fwd_finalize64");
 }
 
-extern "C" int sd_bn_bwd_finalize64(const double* local_sums, const double* global_sums, int C, double count,
-                                    const float* gamma, const float* invstd, int batch_stats, float* dgamma,
+extern "C" int sd_bn_bwd_finalize64(const double* local_sums, const double* global_sums, int C, const float* gamma, const float* invstd, int batch_stats, float* dgamma,
                                     float* dbeta, float* coef, sd_stream s) {
-    SD_REQUIRE(local_sums && global_sums && C > 0 && count > 0 && gamma && invstd && dgamma && dbeta && coef,
+    SD_REQUIRE(local_sums && global_sums && C > 0 && gamma && invstd && dgamma && dbeta && coef,
                "sd_bn_bwd_finalize64: bad args");
     hipLaunchKernelGGL(k_bn_bwd_finalize64, dim3(cdiv(C, 256)), dim3(256), 0, to_stream(s), local_sums, global_sums, C,
-                       count, gamma, invstd, batch_stats, dgamma, dbeta, coef);
+                       gamma, invstd, batch_stats, dgamma, dbeta, coef);
     return sd_check_launch("sd_bn_bwd_finalize64");
 }
 

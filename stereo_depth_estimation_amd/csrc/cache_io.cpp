@@ -1,6 +1,7 @@
 // Native host readers for the data path: the reference's sample cache and its PNG frames.
 // Sample cache (reference dataset.py:86-105 load_cached_sample, cache.py:50-112):
-// one np.savez file per pair, an uncompressed zip of left.npy / right.npy (uint8 HWC) and disparity.npy (f16 HW).
+// one np.savez file per pair, a zip of left.npy / right.npy (uint8 HWC) and disparity.npy (f16 HW): stored members
+// (np.savez, the default) or raw-deflate members (np.savez_compressed, the reference's `cache.py --compress`).
 // A batch of files is read by a pool of threads straight into the caller's (pinned) host buffers, so the data path
 // needs no worker processes, no pickling and no second pinning copy (tools/loader_bench.py: the torch DataLoader
 // path tops out near 3-4k pairs/s on the box's 16 cores).
@@ -81,9 +82,34 @@ bool npy_payload(const unsigned char* p, size_t n, const char* descr, const std:
     return true;
 }
 
-// walks the zip's local headers (np.savez: stored, sizes in the header or its zip64 extra field)
+// a raw-deflate zip member (method 8) inflated into `out` (exactly usize bytes)
+bool inflate_member(const unsigned char* src, size_t csize, size_t usize, std::vector<unsigned char>& out,
+                    std::string& why) {
+    out.resize(usize);
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    if (inflateInit2(&zs, -MAX_WBITS) != Z_OK) {
+        why = "inflateInit2 failed";
+        return false;
+    }
+    zs.next_in = const_cast<unsigned char*>(src);
+    zs.avail_in = (uInt)csize;
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)usize;
+    const int rc = inflate(&zs, Z_FINISH);
+    const size_t got = zs.total_out;
+    inflateEnd(&zs);
+    if (rc != Z_STREAM_END || got != usize) {
+        why = "corrupt deflate member";
+        return false;
+    }
+    return true;
+}
+
+// walks the zip's local headers (sizes in the header or its zip64 extra field); members stored (np.savez) or
+// deflated (np.savez_compressed), inflated into `scratch`
 bool parse_npz(const std::vector<unsigned char>& f, int H, int W, unsigned char* left, unsigned char* right,
-               uint16_t* disp, std::string& why) {
+               uint16_t* disp, std::vector<unsigned char>& scratch, std::string& why) {
     const std::string s3 = "(" + std::to_string(H) + ", " + std::to_string(W) + ", 3)";
     const std::string s2 = "(" + std::to_string(H) + ", " + std::to_string(W) + ")";
     const size_t rgb = (size_t)H * W * 3, dbytes = (size_t)H * W * 2;
@@ -106,29 +132,38 @@ bool parse_npz(const std::vector<unsigned char>& f, int H, int W, unsigned char*
                 k += 4 + sz;
             }
         }
-        if (method != 0 || (flags & 8) || csize != usize) {
-            why = "member " + name + " is compressed or streamed (not np.savez output)";
+        if ((method != 0 && method != 8) || (flags & 8) || (method == 0 && csize != usize)) {
+            why = "member " + name + " uses an unsupported zip method or is streamed (not np.savez output)";
             return false;
         }
         const size_t data = pos + 30 + nlen + xlen;
-        if (data + usize > f.size()) break;
+        if (data + csize > f.size()) break;
+        const bool wanted = name == "left.npy" || name == "right.npy" || name == "disparity.npy";
+        const unsigned char* mem = &f[data];
+        if (wanted && method == 8) {
+            if (usize > ((size_t)1 << 32) || !inflate_member(mem, csize, usize, scratch, why)) {
+                why = name + ": " + (why.empty() ? "member too large" : why);
+                return false;
+            }
+            mem = scratch.data();
+        }
         const unsigned char* src = nullptr;
         if (name == "left.npy" || name == "right.npy") {
-            if (!npy_payload(&f[data], usize, "|u1", s3, rgb, &src, why)) {
+            if (!npy_payload(mem, usize, "|u1", s3, rgb, &src, why)) {
                 why = name + ": " + why;
                 return false;
             }
             memcpy(name[0] == 'l' ? left : right, src, rgb);
             found |= name[0] == 'l' ? 1 : 2;
         } else if (name == "disparity.npy") {
-            if (!npy_payload(&f[data], usize, "<f2", s2, dbytes, &src, why)) {
+            if (!npy_payload(mem, usize, "<f2", s2, dbytes, &src, why)) {
                 why = name + ": " + why;
                 return false;
             }
             memcpy(disp, src, dbytes);
             found |= 4;
         }
-        pos = data + usize;
+        pos = data + csize;
     }
     if (found != 7) {
         why = "missing left/right/disparity member";
@@ -152,11 +187,11 @@ extern "C" int sd_read_cache_batch(const char* const* paths, int n, int H, int W
     std::mutex mu;
     std::string bad_why;
     auto work = [&]() {
-        std::vector<unsigned char> buf;
+        std::vector<unsigned char> buf, scratch;
         std::string why;
         for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) {
             bool ok = paths[i] && read_file(paths[i], buf, why);
-            if (ok) ok = parse_npz(buf, H, W, left + i * rgb, right + i * rgb, disparity + i * hw, why);
+            if (ok) ok = parse_npz(buf, H, W, left + i * rgb, right + i * rgb, disparity + i * hw, scratch, why);
             if (!ok) {
                 std::lock_guard<std::mutex> g(mu);
                 if (i < first_bad.load()) {

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256, RING > 3 ? 1 : 2) void k_convt(const CtArgs p)
 #pragma unroll
             for (int i = 0; i < EI; ++i) {
                 const int q = lane + 64 * i, pl = q / PPX, n8 = (q % PPX) * 8;
-                const unsigned off = last & (mt + pl < p.M) ? (unsigned)((mt + pl) * p.N + n0 + n8) * 2u : OOB;
+                const unsigned off = (last & (mt + pl < p.M)) ? (unsigned)((mt + pl) * p.N + n0 + n8) * 2u : OOB;
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0);
                 yr[i] = make_uint4(v[0], v[1], v[2], v[3]);
             }

@@ -358,6 +358,7 @@ class DeviceLoader:
                                  generator=generator)
         self._stream = None
         self._batches = 0
+        self._seed_drawn = False
 
     def __len__(self) -> int:
         return len(self.loader)
@@ -423,20 +424,46 @@ class DeviceLoader:
         self._h2d_done = [None, None]
 
         def read_png(idxs):  # frames of the un-cached source (pinned by torch's caching host allocator)
-            n = len(idxs)
+            """collate_uint8's groups: one per source frame size, in order of first occurrence in the batch."""
             sm = [samples[i] for i in idxs]
-            hw = png_size(sm[0].left_rgb_path)
-            outs = []
-            for attr in ("left_rgb_path", "right_rgb_path", "disparity_path"):
-                paths = [getattr(x, attr) for x in sm]
-                t = torch.empty(n, *(hw or (1, 1)), 3, dtype=torch.uint8, pin_memory=True)
-                if hw is None or not read_png_batch(paths, hw, t, self.read_threads):
-                    t = torch.from_numpy(np.stack([read_rgb_uint8(p) for p in paths])).pin_memory()
-                outs.append(t)
-            if not (outs[0].shape == outs[1].shape == outs[2].shape):
-                raise ValueError(f"left/right/disparity sizes differ in the batch of {sm[0].disparity_path}")
-            return {"kind": 0, "index": torch.arange(n), "left": outs[0], "right": outs[1], "disparity": outs[2],
-                    "cache_file": [""] * n}
+            attrs = ("left_rgb_path", "right_rgb_path", "disparity_path")
+            by_size: dict = {}
+            for j, x in enumerate(sm):
+                by_size.setdefault(png_size(x.left_rgb_path), []).append(j)
+            parts = []  # (batch positions, left, right, disparity)
+            for hw, pos in by_size.items():
+                outs = []
+                for attr in attrs if hw is not None else ():
+                    t = torch.empty(len(pos), *hw, 3, dtype=torch.uint8, pin_memory=True)
+                    if not read_png_batch([getattr(sm[j], attr) for j in pos], hw, t, self.read_threads):
+                        break
+                    outs.append(t)
+                if len(outs) == 3:
+                    parts.append((pos, *outs))
+                    continue
+                # PIL for these frames (not 8-bit RGB/RGBA PNGs), regrouped by their decoded size
+                dec: dict = {}
+                for j in pos:
+                    f = [read_rgb_uint8(getattr(sm[j], a)) for a in attrs]
+                    if not (f[0].shape == f[1].shape == f[2].shape):
+                        raise ValueError(f"left/right/disparity sizes differ for sample {sm[j].disparity_path}")
+                    dec.setdefault(f[0].shape, []).append((j, f))
+                for items in dec.values():
+                    parts.append(([j for j, _ in items], *(torch.from_numpy(np.stack([f[a] for _, f in items]))
+                                                            .pin_memory() for a in range(3))))
+            first = {}
+            for pos, left, right, disp in parts:  # merge same-size parts, keeping first-occurrence order
+                if not (left.shape == right.shape == disp.shape):
+                    raise ValueError(f"left/right/disparity sizes differ in the batch of {sm[pos[0]].disparity_path}")
+                first.setdefault(tuple(left.shape[1:]), []).append((pos, left, right, disp))
+            groups = []
+            for ps in sorted(first.values(), key=lambda ps: min(min(p[0]) for p in ps)):
+                pos = [j for p in ps for j in p[0]]
+                order = sorted(range(len(pos)), key=lambda i: pos[i])
+                cat = [torch.cat([p[k] for p in ps])[order] if len(ps) > 1 else ps[0][k] for k in (1, 2, 3)]
+                groups.append({"kind": 0, "index": torch.tensor(sorted(pos), dtype=torch.int64), "left": cat[0],
+                               "right": cat[1], "disparity": cat[2], "cache_file": [""] * len(pos)})
+            return groups
 
         def read(k, idxs):
             if root is None:
@@ -445,19 +472,22 @@ class DeviceLoader:
             left, right, disp = (t[:n] for t in bufs[k])
             read_cache_batch([root / sample_cache_relpath(samples[i]) for i in idxs], (H, W), left, right, disp,
                              self.read_threads)
-            return {"kind": 1, "index": torch.arange(n), "left": left, "right": right, "disparity": disp,
-                    "cache_file": [""] * n}
+            return [{"kind": 1, "index": torch.arange(n), "left": left, "right": right, "disparity": disp,
+                     "cache_file": [""] * n}]
 
         with ThreadPoolExecutor(1) as ex:
             # a DataLoader iterator draws its workers' base seed from the generator (or the global RNG) before the
-            # sampler's permutation: the same draw keeps the shuffle order, and the RNG stream after it, identical
-            torch.empty((), dtype=torch.int64).random_(generator=self.loader.generator)
+            # sampler's permutation: the same draw keeps the shuffle order, and the RNG stream after it, identical.
+            # A persistent-workers DataLoader draws it once, when it first creates its iterator (_reset draws no more)
+            if not (self.loader.persistent_workers and self._seed_drawn):
+                torch.empty((), dtype=torch.int64).random_(generator=self.loader.generator)
+                self._seed_drawn = True
             it = iter(self.loader.batch_sampler)
             nxt = next(it, None)
             fut = ex.submit(read, 0, nxt) if nxt is not None else None
             k = 0
             while fut is not None:
-                g = fut.result()
+                gs = fut.result()
                 nxt = next(it, None)
                 fut = None
                 if nxt is not None:
@@ -466,13 +496,15 @@ class DeviceLoader:
                     fut = ex.submit(read, k ^ 1, nxt)
                 if self.dataset.augment:
                     # drawn here, as batch k is handed over, so the main-process RNG sees the order of a
-                    # num_workers=0 DataLoader: factors of batch k (per item, in __getitem__'s calls), then the
-                    # noise seed _prepare draws for batch k, then batch k+1's factors
+                    # num_workers=0 DataLoader: factors of batch k (per item in batch order, in __getitem__'s calls),
+                    # then the noise seeds _prepare draws for batch k's groups, then batch k+1's factors
                     ds = self.dataset
-                    g["aug"] = torch.from_numpy(np.stack([np.stack([ds.sample_augment_params(), ds.sample_augment_params()])
-                                                          for _ in range(len(g["index"]))]))
+                    n = sum(len(g["index"]) for g in gs)
+                    aug = np.stack([np.stack([ds.sample_augment_params(), ds.sample_augment_params()]) for _ in range(n)])
+                    for g in gs:
+                        g["aug"] = torch.from_numpy(aug[g["index"].numpy()])
                 self._slot = k
-                yield [g]
+                yield gs
                 k ^= 1
 
     def __iter__(self):

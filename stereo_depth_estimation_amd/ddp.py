@@ -61,6 +61,9 @@ class BucketAllReduce:
         self.flat, self.buckets, self.group = flat, buckets, group
         self.last_of = {names[-1]: i for i, (names, _, _) in enumerate(buckets)}
         self.handles = []
+        # measurement (bench.py): (start, end) HIP events around each wait, on the stream that waits. With RCCL the
+        # wait makes the current stream wait for RCCL's, so end - start is the all-reduce time backward did not hide
+        self.wait_events: list | None = None
 
     def on_grads_ready(self, name: str):
         i = self.last_of.get(name)
@@ -69,16 +72,39 @@ class BucketAllReduce:
             self.handles.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def wait(self):
+        ev = None
+        if self.wait_events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for h in self.handles:
             h.wait()
         self.handles.clear()
+        if ev is not None:
+            ev[1].record()
+            self.wait_events.append(ev)
+
+
+class ShardSampler(torch.utils.data.Sampler):
+    """Exact, unpadded shard of a dataset for evaluation: rank r takes indices r, r + world, ... . Every sample is
+    seen by exactly one rank, so the all-reduced metric sums equal the single-process epoch's (the reference's
+    validation, train.py:617-620), where torch's DistributedSampler pads the shards with repeated samples."""
+
+    def __init__(self, n: int, world: int, rank: int):
+        self.n, self.world, self.rank = n, world, rank
+
+    def __iter__(self):
+        return iter(range(self.rank, self.n, self.world))
+
+    def __len__(self) -> int:
+        return len(range(self.rank, self.n, self.world))
 
 
 class DataParallel:
     def __init__(self, model, group=None, bucket_cap_mb: float = 8.0, broadcast: bool = True, sync_bn: bool = False):
         """sync_bn: global-batch BatchNorm statistics (torch.nn.SyncBatchNorm semantics; SURVEY §8e "--sync-bn"):
         one fp64 all-reduce of per-channel (sum, sumsq) per BN layer in the forward and of (sum dz, sum dz*xhat) in
-        the backward, 2 x 18 small collectives per step. Needs equal batch shapes on every rank."""
+        the backward, 2 x 18 small collectives per step. Each carries the rank's pixel count, so ranks may hold
+        batches of different sizes (the last batch of an epoch)."""
         self.model, self.group = model, group
         self.world = dist.get_world_size(group)
         self.cap = int(bucket_cap_mb * 1024 * 1024 / 4)
@@ -89,7 +115,6 @@ class DataParallel:
         if sync_bn:
             eng = model.engine(next(model.parameters()).device)
             eng.bn_sync = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-            eng.bn_world = self.world
 
     def broadcast_state(self):
         dev = next(self.model.parameters()).device
@@ -115,7 +140,9 @@ class DataParallel:
         from .train import train_step
 
         if optimizer is None:
-            train_step(model, None, inputs, targets, valid_mask, count_hook=self._allreduce_count)
+            # evaluation: no loss normaliser is needed (the metric sums count this rank's pixels, summed once per epoch
+            # by sum_metrics), so no per-batch collective either: ranks may hold different numbers of batches
+            train_step(model, None, inputs, targets, valid_mask)
             return
         ar = self._reducer()
         train_step(model, optimizer, inputs, targets, valid_mask, grad_hook=ar.on_grads_ready,

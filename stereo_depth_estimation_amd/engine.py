@@ -169,9 +169,8 @@ class UNetEngine:
         self._slab_free: list = [None, None]
         self._slab_i = 0
         # SyncBatchNorm (ddp.DataParallel(sync_bn=True)): bn_sync(t) SUM-all-reduces an fp64 device tensor in stream
-        # order; bn_world ranks with equal per-rank batch shapes. None: per-rank BatchNorm statistics.
+        # order (the per-channel sums and each rank's pixel count). None: per-rank BatchNorm statistics.
         self.bn_sync = None
-        self.bn_world = 1
         self._bn64: torch.Tensor | None = None
         self.params: dict[str, torch.Tensor] = {}
         self.grads: dict[str, torch.Tensor] = {}
@@ -369,10 +368,10 @@ class UNetEngine:
             rows = L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cout)
             rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
             nbt = self.bufs.get(cl.bn_key + ".num_batches_tracked")
-            if self.bn_sync is not None:  # global batch statistics (torch SyncBatchNorm)
-                sums = self._sync_sums(stats, rows, cl.cout)[0]
-                L.call("sd_bn_fwd_finalize64", sums.data_ptr(), cl.cout, float(ws.B * Hl * Wl * self.bn_world),
-                       g.data_ptr(), b.data_ptr(), rm.data_ptr(), rv.data_ptr(), L.ptr(nbt), BN_MOMENTUM, BN_EPS,
+            if self.bn_sync is not None:  # global batch statistics (torch SyncBatchNorm) over the global count
+                sums = self._sync_sums(stats, rows, cl.cout, ws.B * Hl * Wl)[0]
+                L.call("sd_bn_fwd_finalize64", sums.data_ptr(), cl.cout, g.data_ptr(), b.data_ptr(), rm.data_ptr(),
+                       rv.data_ptr(), L.ptr(nbt), BN_MOMENTUM, BN_EPS,
                        mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
             else:
                 L.call("sd_bn_fwd_finalize", stats.data_ptr(), rows, cl.cout, float(ws.B * Hl * Wl), g.data_ptr(),
@@ -567,8 +566,8 @@ class UNetEngine:
             rows = L.call("sd_chan_reduce_rows", P, cl.cout)
         coef = t["coef:" + cl.name]
         if self.bn_sync is not None and ws.fwd_train:
-            loc, glob = self._sync_sums(chan, rows, cl.cout, keep_local=True)
-            L.call("sd_bn_bwd_finalize64", loc.data_ptr(), glob.data_ptr(), cl.cout, float(P * self.bn_world),
+            loc, glob = self._sync_sums(chan, rows, cl.cout, P, keep_local=True)
+            L.call("sd_bn_bwd_finalize64", loc.data_ptr(), glob.data_ptr(), cl.cout,
                    self.params[cl.bn_key + ".weight"].data_ptr(), t["invstd:" + cl.name].data_ptr(), 1,
                    self.grads[cl.bn_key + ".weight"].data_ptr(), self.grads[cl.bn_key + ".bias"].data_ptr(),
                    coef.data_ptr(), s)
@@ -581,15 +580,16 @@ class UNetEngine:
             L.call("sd_bn_bwd_apply", dt, t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), *args,
                    coef.data_ptr(), P, cl.cout, t["dy:" + cl.name].data_ptr(), s)
 
-    def _sync_sums(self, rows_t: torch.Tensor, rows: int, C: int, keep_local: bool = False):
-        """SyncBatchNorm: this rank's float2 partial rows -> fp64 per-channel sums, SUM-all-reduced over the ranks
-        (stream-ordered). Returns (global, _) or, with keep_local, (local, global)."""
+    def _sync_sums(self, rows_t: torch.Tensor, rows: int, C: int, pixels: int, keep_local: bool = False):
+        """SyncBatchNorm: this rank's float2 partial rows -> fp64 per-channel sums plus its pixel count, SUM-all-reduced
+        over the ranks (stream-ordered), so the finalizes divide by the global count even when the ranks' batches
+        differ. Returns (global, _) or, with keep_local, (local, global)."""
         if C > 2048:
             raise ValueError(f"SyncBatchNorm: {C} channels > 2048")
         if self._bn64 is None or self._bn64.device != self.device:
-            self._bn64 = torch.empty(2, 2 * 2048, dtype=torch.float64, device=self.device)
-        loc, glob = self._bn64[0, :2 * C], self._bn64[1, :2 * C]
-        L.call("sd_bn_rows_sum64", rows_t.data_ptr(), rows, C, loc.data_ptr(), self._s())
+            self._bn64 = torch.empty(2, 2 * 2048 + 1, dtype=torch.float64, device=self.device)
+        loc, glob = self._bn64[0, :2 * C + 1], self._bn64[1, :2 * C + 1]
+        L.call("sd_bn_rows_sum64", rows_t.data_ptr(), rows, C, float(pixels), loc.data_ptr(), self._s())
         if not keep_local:
             self.bn_sync(loc)
             return loc, None

@@ -204,10 +204,39 @@ def gen_data():
     np.savez_compressed(OUT / "data_path.npz", **out)
 
 
+def gen_bf16():
+    """The reference's own bf16 behaviour: the same full-size forwards and train step as
+    gen_full, run under torch.autocast("cpu", dtype=torch.bfloat16). The drift of these outputs from the fp32
+    ones is the yardstick the HIP bf16 path's bounds are calibrated to (tests/test_gpu_model.py)."""
+    base = 32
+    state = make_state(base, seed=3)
+    out = {}
+    m = build_ref(base, state).eval()
+    b = make_batch(1, 240, 320, seed=4)
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+        d, lv = m(torch.as_tensor(b["input"]), return_uncertainty=True)
+    out["eval_disp"], out["eval_logvar"] = d.float().numpy(), lv.float().numpy()
+    m = build_ref(base, state)
+    b = make_batch(2, 240, 320, seed=6)
+    mc = copy.deepcopy(m).train()
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+        d, lv = mc(torch.as_tensor(b["input"]), return_uncertainty=True)
+    out["train_fwd_disp"], out["train_fwd_logvar"] = d.float().numpy(), lv.float().numpy()
+    names = trainable_named(m)
+    opt = RecordingAdamW([p for _, p in names], names, lr=1e-3, weight_decay=1e-4)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        metrics, _ = ref_train.run_epoch(m, [batch_to_torch(b)], torch.device("cpu"), optimizer=opt, global_step=0)
+    for k, v in metrics.items():
+        out["metrics/" + k] = np.float64(v)
+    for k, g in opt.grads[0].items():
+        out["gnorm/" + k] = np.float64(g.double().norm().item())
+    np.savez_compressed(OUT / "full_bf16.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    gen_data()
-    gen_tiny()
-    gen_full()
+    parts = sys.argv[1:] or ["data", "tiny", "full", "bf16"]
+    for part in parts:
+        {"data": gen_data, "tiny": gen_tiny, "full": gen_full, "bf16": gen_bf16}[part]()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)

@@ -143,7 +143,8 @@ def test_collate_groups_by_kind_and_size(tmp_path):
 def test_native_cache_reader_matches_numpy_load(tmp_path):
     """sd_read_cache_batch (host C++, no GPU) returns exactly what the reference's load_cached_sample reads with
     np.load from files in its format (save_cached_sample = reference dataset.py:108-128), and rejects what the
-    reference would: a missing entry, another image size, a non-savez (compressed) file."""
+    reference would: a missing entry, another image size. Caches written with the reference's `cache.py --compress`
+    (np.savez_compressed: deflated zip members) load too, as np.load reads them."""
     rng = np.random.default_rng(3)
     H, W, n = 24, 32, 5
     paths, ref = [], []
@@ -168,10 +169,21 @@ def test_native_cache_reader_matches_numpy_load(tmp_path):
     with pytest.raises(ValueError, match="shape-mismatched"):
         D.read_cache_batch(paths[:1], (H, W + 8), torch.empty(1, H, W + 8, 3, dtype=torch.uint8),
                            torch.empty(1, H, W + 8, 3, dtype=torch.uint8), torch.empty(1, H, W + 8, dtype=torch.int16))
-    comp = tmp_path / "compressed.npz"
-    np.savez_compressed(comp, left=ref[0][0], right=ref[0][1], disparity=ref[0][2])
-    with pytest.raises(ValueError, match="compressed"):
-        D.read_cache_batch([comp], (H, W), lt[:1], rt[:1], dt[:1])
+    comp = []
+    for i, (l_, r_, d_) in enumerate(ref):
+        comp.append(tmp_path / f"compressed{i}.npz")
+        np.savez_compressed(comp[-1], left=l_, right=r_, disparity=d_)
+    lt.zero_(), rt.zero_(), dt.zero_()
+    D.read_cache_batch(comp[:2] + paths[2:], (H, W), lt, rt, dt, threads=2)  # mixed stored / deflated files
+    for i, (l_, r_, d_) in enumerate(ref):
+        assert np.array_equal(lt[i].numpy(), l_) and np.array_equal(rt[i].numpy(), r_)
+        assert np.array_equal(dt[i].numpy().view(np.float16), d_)
+    bad = tmp_path / "corrupt.npz"
+    raw = bytearray(comp[0].read_bytes())
+    raw[60:90] = bytes(30)  # clobber the first deflate stream
+    bad.write_bytes(bytes(raw))
+    with pytest.raises(ValueError):
+        D.read_cache_batch([bad], (H, W), lt[:1], rt[:1], dt[:1])
 
 
 def _png_with_filters(path, img):

@@ -1,0 +1,252 @@
+"""BASELINE.json's GPU configs through the product kernels, with bf16 / fp8 bounds calibrated to the reference's
+OWN reduced-precision behaviour (needs an MI355X).
+
+Yardstick: the reference run under ``torch.autocast("cpu", dtype=torch.bfloat16)`` on the same weights and inputs
+(`tests/golden/full_bf16.npz`, written by gen_golden.py from the reference itself at 240x320; recomputed here with
+the oracle at the other sizes). Its drift from the fp32 reference is what "bf16 numerics" costs the reference; the
+HIP bf16 path (bf16 activations, fp32 accumulation) must stay within that drift, times the factor each test states:
+
+  eval forward (running statistics)   max and mean |Δ| <= 1.0x autocast   (measured 0.06x / 0.03x at 240x320)
+  train forward (batch statistics)    max and mean |Δ| <= 1.5x autocast   (measured 0.82x / 0.92x)
+  train step                          loss metrics rel. error <= autocast's (floor 1e-6);
+                                      per-tensor grad-norm rel. error: median <= 1.5x and max <= 1.5x autocast's
+  fp8 e4m3 eval forward (960x720)     max <= 6x, mean <= 4x the bf16 autocast drift (e4m3 keeps 3 mantissa bits
+                                      to bf16's 7; measured 0.9x-4.2x max, 0.3x-2.6x mean)
+fp32 stays at the north star's per-pixel |Δ| < 1e-3 (measured 6e-8 at 960x720).
+Configs: C2 = 320x240 B=64 train step; C4 = 640x480 train step; C5 = 960x720 B=1 eval forward (live app).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_ref as U
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.set_num_threads(16)
+
+
+def _hip_model(state, precision):
+    from stereo_depth_estimation_amd.model import StereoUNet
+
+    m = StereoUNet(base_channels=32, precision=precision)
+    m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in state.items()}, strict=True)
+    return m.to(DEV)
+
+
+def _drift(got, ref):
+    d = (torch.as_tensor(np.asarray(got)).double() - torch.as_tensor(np.asarray(ref)).double()).abs()
+    return float(d.max()), float(d.mean())
+
+
+def _assert_within(name, got, ref, ac, fmax, fmean):
+    gmax, gmean = _drift(got, ref)
+    amax, amean = _drift(ac, ref)
+    assert gmax <= fmax * amax, f"{name}: max |Δ| {gmax:.3g} > {fmax} x autocast {amax:.3g}"
+    assert gmean <= fmean * amean, f"{name}: mean |Δ| {gmean:.3g} > {fmean} x autocast {amean:.3g}"
+
+
+def _hip_step(state, precision, batch):
+    """One fused train step (run_epoch): (metrics, per-tensor gradient norms before AdamW)."""
+    from stereo_depth_estimation_amd.optim import FusedAdamW
+    from stereo_depth_estimation_amd.train import run_epoch
+
+    m = _hip_model(state, precision)
+    opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    gn = {}
+    orig = opt.fused_step
+
+    def rec(**kw):
+        if not gn:
+            torch.cuda.synchronize()
+            gn.update({k: float(v.detach().double().norm()) for k, v in m._grad_views.items()})
+        orig(**kw)
+
+    opt.fused_step = rec
+    bd = {k: torch.as_tensor(np.asarray(v)).to(DEV) for k, v in batch.items()}
+    metrics, _ = run_epoch(m, [bd], torch.device(DEV), optimizer=opt)
+    return metrics, gn
+
+
+def _oracle_step(state, batch, autocast=False):
+    net = U.Net(state)
+    opt = U.AdamWState(net.trainable())
+    gn = {}
+    orig = opt.step
+
+    def rec(params):
+        params = list(params)
+        gn.update({k: float(p.grad.double().norm()) for k, p in params})
+        orig(params)
+
+    opt.step = rec
+    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+        metrics, _ = U.run_epoch(net, [batch], opt)
+    return metrics, gn
+
+
+def _rel(a, b):
+    return {k: abs(a[k] - b[k]) / (abs(b[k]) + 1e-12) for k in b}
+
+
+def _assert_step_within(got, ref, ac, gfactor=1.5):
+    """got/ref/ac: (metrics, grad norms) of the HIP bf16 step, the fp32 reference and the autocast reference."""
+    em, am = _rel(got[0], ref[0]), _rel(ac[0], ref[0])
+    for k in ref[0]:
+        assert em[k] <= max(am[k], 1e-6), (k, em[k], am[k])
+    eg, ag = _rel(got[1], ref[1]), _rel(ac[1], ref[1])
+    hmed, amed = float(np.median(list(eg.values()))), float(np.median(list(ag.values())))
+    worst = max(eg, key=eg.get)
+    assert hmed <= gfactor * amed, ("median grad-norm error", hmed, amed)
+    assert eg[worst] <= gfactor * max(ag.values()), ("worst grad-norm error", worst, eg[worst], max(ag.values()))
+
+
+# ---------------------------------------------------------------------------------------------- 240x320 goldens
+def test_bf16_eval_forward_within_reference_autocast_drift(golden_dir):
+    ev, ac = np.load(golden_dir / "full_eval.npz"), np.load(golden_dir / "full_bf16.npz")
+    m = _hip_model(U.make_state(32, seed=3), "bf16").eval()
+    x = torch.as_tensor(U.make_batch(1, 240, 320, seed=4)["input"]).to(DEV)
+    with torch.no_grad():
+        d, lv = m(x, return_uncertainty=True)
+    _assert_within("disp", d.cpu(), ev["disp"], ac["eval_disp"], 1.0, 1.0)
+    _assert_within("logvar", lv.cpu(), ev["logvar"], ac["eval_logvar"], 1.0, 1.0)
+
+
+def test_bf16_train_forward_within_reference_autocast_drift(golden_dir):
+    tr, ac = np.load(golden_dir / "full_train.npz"), np.load(golden_dir / "full_bf16.npz")
+    m = _hip_model(U.make_state(32, seed=3), "bf16").train()
+    x = torch.as_tensor(U.make_batch(2, 240, 320, seed=6)["input"]).to(DEV)
+    with torch.no_grad():
+        d, lv = m(x, return_uncertainty=True)
+    _assert_within("disp", d.cpu(), tr["train_fwd_disp"], ac["train_fwd_disp"], 1.5, 1.5)
+    _assert_within("logvar", lv.cpu(), tr["train_fwd_logvar"], ac["train_fwd_logvar"], 1.5, 1.5)
+
+
+def _golden_step(g):
+    return ({k[8:]: float(g[k]) for k in g.files if k.startswith("metrics/")},
+            {k[6:]: float(g[k]) for k in g.files if k.startswith("gnorm/")})
+
+
+def test_bf16_train_step_within_reference_autocast_drift(golden_dir):
+    tr, ac = np.load(golden_dir / "full_train.npz"), np.load(golden_dir / "full_bf16.npz")
+    got = _hip_step(U.make_state(32, seed=3), "bf16", U.make_batch(2, 240, 320, seed=6))
+    _assert_step_within(got, _golden_step(tr), _golden_step(ac))
+
+
+# ---------------------------------------------------------------------------------------------- C4: 640x480
+def test_c4_640x480_train_step_fp32_and_bf16_vs_oracle():
+    """BASELINE config 4's resolution: one train step (forward, loss, backward; B=2) at 640x480. fp32: metrics to
+    1e-4 and per-tensor grad norms to 5e-3 of the oracle's fp32 step (test_gpu_model's full-size bounds); bf16: within
+    the oracle's own autocast drift on the same batch."""
+    st = U.make_state(32, seed=3)
+    b = U.make_batch(2, 480, 640, seed=12)
+    ref = _oracle_step(st, b)
+    ac = _oracle_step(st, b, autocast=True)
+    m32, g32 = _hip_step(st, "fp32", b)
+    for k, v in ref[0].items():
+        assert abs(m32[k] - v) <= 1e-4 * abs(v), (k, m32[k], v)
+    for k, v in ref[1].items():
+        assert abs(g32[k] - v) <= 5e-3 * v + 1e-7, (k, g32[k], v)
+    _assert_step_within(_hip_step(st, "bf16", b), ref, ac)
+
+
+# ---------------------------------------------------------------------------------------------- C5: 960x720
+def test_c5_960x720_eval_forward_fp32_bf16_fp8_vs_oracle():
+    """BASELINE config 5 (the live app's forward, depth_live_dl.py:516-529: B=1, eval BN, both heads) at 960x720:
+    fp32 per-pixel < 1e-3; bf16 within the oracle's autocast drift; fp8 within 6x / 4x of it (module docstring)."""
+    st = U.make_state(32, seed=3)
+    x = torch.as_tensor(U.make_batch(1, 720, 960, seed=13)["input"])
+    net = U.Net(st)
+    with torch.no_grad():
+        d_ref, lv_ref = net.forward(x, train=False)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            d_ac, lv_ac = net.forward(x, train=False)
+    d_ac, lv_ac = d_ac.float(), lv_ac.float()
+    out = {}
+    for prec in ("fp32", "bf16", "fp8"):
+        m = _hip_model(st, prec).eval()
+        with torch.inference_mode():
+            d, lv = m(x.to(DEV), return_uncertainty=True)
+        out[prec] = (d.cpu(), lv.cpu())
+    assert float((out["fp32"][0] - d_ref).abs().max()) < 1e-3
+    assert float((out["fp32"][1] - lv_ref).abs().max()) < 1e-3
+    _assert_within("bf16 disp", out["bf16"][0], d_ref, d_ac, 1.0, 1.0)
+    _assert_within("bf16 logvar", out["bf16"][1], lv_ref, lv_ac, 1.0, 1.0)
+    _assert_within("fp8 disp", out["fp8"][0], d_ref, d_ac, 6.0, 4.0)
+    _assert_within("fp8 logvar", out["fp8"][1], lv_ref, lv_ac, 6.0, 4.0)
+
+
+# ---------------------------------------------------------------------------------------------- C2: B=64
+def test_c2_batch64_train_step_bf16_vs_oracle_and_fp32(golden_dir):
+    """BASELINE config 2's batch (64 pairs at 320x240; the bench's workload, whose split-K counts, slab sizes and
+    persistent-grid item counts differ from B=2): loss metrics of the bf16 step vs the oracle's train-mode forward on
+    the same synthetic batch (within the reference autocast's metric drift from full_bf16.npz, floor 1e-6); fp32
+    metrics to 1e-5; bf16 gradient norms vs the fp32 HIP step (pinned to the reference above) within autocast's
+    grad-norm drift (median and worst tensor)."""
+    from stereo_depth_estimation_amd.data import synthetic_batch
+
+    tr, acg = np.load(golden_dir / "full_train.npz"), np.load(golden_dir / "full_bf16.npz")
+    ref_full, ac_full = _golden_step(tr), _golden_step(acg)
+    ac_m, ac_g = _rel(ac_full[0], ref_full[0]), _rel(ac_full[1], ref_full[1])
+    st = U.make_state(32, seed=3)
+    b = {k: v.numpy() for k, v in synthetic_batch(64, 240, 320, seed=21).items()}
+    m16, g16 = _hip_step(st, "bf16", b)
+    m32, g32 = _hip_step(st, "fp32", b)
+    net = U.Net(st)
+    with torch.no_grad():
+        d, lv = net.forward(torch.as_tensor(b["input"]), train=True)
+        _, s = U.masked_nll(d, lv, torch.as_tensor(b["target"]), torch.as_tensor(b["valid_mask"]))
+    n = s["n"]
+    ref = {"loss": s["nll"] / n, "mae": s["abs"] / n, "rmse": (s["sq"] / n) ** 0.5, "sigma": s["sigma"] / n}
+    for k, v in ref.items():
+        assert abs(m32[k] - v) <= 1e-5 * abs(v), ("fp32", k, m32[k], v)
+        assert abs(m16[k] - v) <= max(ac_m[k], 1e-6) * abs(v), ("bf16", k, m16[k], v, ac_m[k])
+    e = _rel(g16, g32)
+    assert float(np.median(list(e.values()))) <= float(np.median(list(ac_g.values())))
+    assert max(e.values()) <= max(ac_g.values()), max(e.items(), key=lambda kv: kv[1])
+
+
+# ---------------------------------------------------------------------------------------------- EPE, trained model
+def test_epe_bf16_and_fp32_vs_oracle_on_trained_checkpoint():
+    """North star: "disparity EPE within 1e-3 of reference". EPE is the reference's `mae` (train.py:350,406): mean
+    |disparity - target| over valid pixels in the validation epoch (eval-mode BN, train.py:301). A bf16 model is
+    trained on synthetic rectified pairs until its disparity tracks the targets; then the same checkpoint is
+    evaluated on held-out pairs by the bf16 path, the fp32 path and the CPU oracle (the reference's arithmetic), in
+    fp32 and under torch.autocast(bf16). Bounds: |EPE_fp32 - EPE_ref| < 1e-5 px; |EPE_bf16 - EPE_ref| below the
+    north star's 1e-3 px or the reference's own autocast EPE shift, whichever is larger. (Training uses lr 5e-3 so
+    that 400 steps reach the targets' scale; the optimizer is not what is tested here.)"""
+    from stereo_depth_estimation_amd.data import synthetic_batch
+    from stereo_depth_estimation_amd.model import StereoUNet
+    from stereo_depth_estimation_amd.optim import FusedAdamW
+    from stereo_depth_estimation_amd.train import run_epoch, train_step
+
+    torch.manual_seed(42)
+    m = StereoUNet(precision="bf16").to(DEV).train()
+    opt = FusedAdamW(m.parameters(), lr=5e-3, weight_decay=1e-4)
+    train = [synthetic_batch(32, 240, 320, seed=700 + i, device=DEV) for i in range(8)]
+    val = synthetic_batch(4, 240, 320, seed=999, device=DEV)
+    e0 = run_epoch(m, [val], torch.device(DEV))[0]["mae"]
+    m.train()
+    for i in range(400):
+        b = train[i % len(train)]
+        train_step(m, opt, b["input"], b["target"], b["valid_mask"])
+    e16 = run_epoch(m, [val], torch.device(DEV))[0]["mae"]
+    m32 = StereoUNet(precision="fp32").to(DEV)
+    m32.load_state_dict(m.state_dict())
+    e32 = run_epoch(m32, [val], torch.device(DEV))[0]["mae"]
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    vb = [{k: v.cpu().numpy() for k, v in val.items()}]
+    ref, _ = U.run_epoch(U.Net(sd), vb, None)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ac, _ = U.run_epoch(U.Net(sd), vb, None)
+    print(f"EPE: init {e0:.4f}, bf16 {e16:.6f}, fp32 {e32:.6f}, oracle {ref['mae']:.6f}, oracle autocast {ac['mae']:.6f}")
+    assert e16 < 0.5 * e0, ("the model did not train", e0, e16)
+    assert abs(e32 - ref["mae"]) < 1e-5, (e32, ref["mae"])
+    assert abs(e16 - ref["mae"]) < max(1e-3, abs(ac["mae"] - ref["mae"])), (e16, ref["mae"], ac["mae"])

@@ -94,7 +94,7 @@ def _worker(rank: int, world: int, port: int, q, backend: str = "gloo"):
         synced = all(torch.equal(gathered[0], g) for g in gathered)
         q.put((rank, diff, moved, in_sync and drifted and synced, None))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, None, None, None, None, repr(e)))
+        q.put((rank, None, None, None, repr(e)))
         raise
     finally:
         dist.destroy_process_group()
@@ -169,7 +169,7 @@ def _sync_bn_worker(rank: int, world: int, port: int, q, precision: str = "fp32"
               f"running stats rel {bdiff:.3e} (per-rank BN {bctrl:.3e})", flush=True)
         q.put((rank, diff, bdiff, ctrl, bctrl, None))
     except Exception as e:
-        q.put((rank, None, None, None, None, repr(e)))
+        q.put((rank, None, None, None, repr(e)))
         raise
     finally:
         dist.destroy_process_group()

@@ -10,9 +10,9 @@ Tolerances (stated per BASELINE.json north_star):
               AdamW updates after 2 steps: >= 99.9 % of elements within 2e-5 of the reference and all
               within 4e-3 (= 2 steps x 2 x lr: Adam's m/sqrt(v) turns fp32 noise in near-zero
               gradients into O(lr) update differences, as it does in the reference's own fp32 run)
-  bf16 mode : bf16 storage drifts ~2e-3 at init even under torch autocast (SURVEY §0);
-              we assert per-pixel |Δ| < 0.1·(1+|ref|) and mean |Δ| < 5e-3·mean|ref|, and loss-metric
-              agreement to 2 %.
+  bf16 mode : bounded by the reference's OWN drift under torch.autocast(bf16) on the same inputs (SURVEY §0
+              measured 2.1e-3 at init); see tests/test_gpu_configs.py for the calibrated forward / train-step
+              bounds at 240x320, 640x480 (C4), 960x720 (C5) and B=64 (C2).
 """
 
 import math
@@ -244,21 +244,6 @@ def test_autograd_path_matches_fused_path():
         assert float(np.abs(got - ref).max()) / scale < 1e-3, k
 
 
-def test_bf16_tiny_and_full_forward_close():
-    st = U.make_state(32, seed=3)
-    b = U.make_batch(2, 240, 320, seed=6)
-    net = U.Net(st)
-    with torch.no_grad():
-        d_ref, lv_ref = net.forward(torch.as_tensor(b["input"]), train=True)
-    m = _hip_model(st, 32, "bf16").train()
-    with torch.no_grad():
-        d, lv = m(torch.as_tensor(b["input"]).to(DEV), return_uncertainty=True)
-    for got, ref in ((d.cpu(), d_ref), (lv.cpu(), lv_ref)):
-        err = (got - ref).abs()
-        assert float((err / (1 + ref.abs())).max()) < 0.1
-        assert float(err.mean()) < 5e-3 * float(ref.abs().mean()) + 5e-3
-
-
 @pytest.mark.parametrize("precision", ["bf16", "fp8"])
 def test_eval_forward_reuses_packs_and_tracks_weight_changes(precision):
     """Eval forwards skip re-packing weights and recomputing BN coefficients while the state is
@@ -316,7 +301,8 @@ def test_eval_forward_reuses_packs_and_tracks_weight_changes(precision):
 
 def test_640x480_forward_fp32_and_bf16_vs_oracle():
     """BASELINE config 4's resolution (640x480): the fp32 eval forward within the north star's per-pixel 1e-3 of the
-    CPU restatement, and the bf16 train-mode forward (batch statistics) within the bf16 bounds above."""
+    CPU restatement, and the bf16 train-mode forward (batch statistics) within 1.5x the oracle's own autocast(bf16)
+    drift on the same batch (max and mean; measured 0.8-0.9x at 240x320)."""
     st = U.make_state(32, seed=3)
     b = U.make_batch(2, 480, 640, seed=12)
     net = U.Net(st)
@@ -324,6 +310,8 @@ def test_640x480_forward_fp32_and_bf16_vs_oracle():
     with torch.no_grad():
         d_ev, lv_ev = net.forward(x[:1], train=False)
         d_tr, lv_tr = net.forward(x, train=True)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            d_ac, lv_ac = U.Net(st).forward(x, train=True)
     m = _hip_model(st, 32, "fp32").eval()
     with torch.no_grad():
         d, lv = m(x[:1].to(DEV), return_uncertainty=True)
@@ -332,7 +320,7 @@ def test_640x480_forward_fp32_and_bf16_vs_oracle():
     m = _hip_model(st, 32, "bf16").train()
     with torch.no_grad():
         d, lv = m(x.to(DEV), return_uncertainty=True)
-    for got, ref in ((d.cpu(), d_tr), (lv.cpu(), lv_tr)):
-        err = (got - ref).abs()
-        assert float((err / (1 + ref.abs())).max()) < 0.1
-        assert float(err.mean()) < 5e-3 * float(ref.abs().mean()) + 5e-3
+    for got, ref, ac in ((d.cpu(), d_tr, d_ac.float()), (lv.cpu(), lv_tr, lv_ac.float())):
+        err, drift = (got - ref).abs(), (ac - ref).abs()
+        assert float(err.max()) <= 1.5 * float(drift.max()), (float(err.max()), float(drift.max()))
+        assert float(err.mean()) <= 1.5 * float(drift.mean()), (float(err.mean()), float(drift.mean()))

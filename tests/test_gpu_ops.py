@@ -27,7 +27,7 @@ def L():
 
 def _tol(ref, prec):
     m = float(ref.abs().max())
-    return (1e-4 if prec == "fp32" else 2e-2) * (1 + m)
+    return (1e-4 if prec == "fp32" else 5e-3) * (1 + m)
 
 
 def _adt(prec):

@@ -65,8 +65,15 @@ def main(fetch_csv: str, write_csv: str):
         res[k] = {"launches_fetch_pass": nf, "launches_write_pass": nw, "read_bytes_per_launch": rd,
                   "write_bytes_per_launch": wr,
                   "hbm_bytes_per_launch": (rd or 0.0) + (wr or 0.0) if rd is not None and wr is not None else None}
+    import hashlib
+    import os
+
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "stereo_depth_estimation_amd", "libstereo_hip.so")
+    with open(lib, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    # bench.py reports a kernel's traffic only when this matches the library it loaded (same build)
     json.dump({"source": [fetch_csv, write_csv], "correction": "bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE)",
-               "kernels": res}, sys.stdout, indent=1)
+               "lib_sha256": sha, "kernels": res}, sys.stdout, indent=1)
     print()
 
 
