@@ -20,5 +20,5 @@ rc=$?; echo "bench exit $rc" | tee -a "$OUT/status.txt"; [ $rc -eq 0 ] || exit $
 cat "$OUT/bench.json"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-infer > "$OUT/prof.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-infer --epe-steps 0 > "$OUT/prof.log" 2>&1
 rc=$?; echo "rocprof exit $rc" | tee -a "$OUT/status.txt"; exit $rc

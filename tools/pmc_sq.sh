@@ -13,6 +13,6 @@ for c in SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLIC
 done
 timeout -k 10 240 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT \
     SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq" -o sq -- \
-    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-infer --no-roofline > "$OUT/sq.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-infer --no-roofline --epe-steps 0 > "$OUT/sq.log" 2>&1
 rc=$?; echo "sq exit $rc" | tee -a "$OUT/status.txt"; [ $rc -eq 0 ] || exit $rc
 cd "$ROOT" && python3 tools/pmc_sq.py $(ls "$OUT"/sq/*counter_collection.csv) $(ls "$OUT"/sq/*kernel_trace.csv) > "$OUT/pmc_sq.json"
