@@ -16,7 +16,7 @@ for arm in new old new2 old2; do
 done
 for arm in new old new2 old2; do
     case $arm in old*) export SD_HIP_LIB=$OLD ;; *) unset SD_HIP_LIB ;; esac
-    timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-infer > "$OUT/bench_$arm.json" 2> "$OUT/bench_$arm.err" || exit 4
+    timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-infer --epe-steps 0 > "$OUT/bench_$arm.json" 2> "$OUT/bench_$arm.err" || exit 4
 done
 unset SD_HIP_LIB
 python tools/ab_summary.py "$OUT"
