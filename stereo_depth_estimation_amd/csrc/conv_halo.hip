@@ -226,6 +226,8 @@ __host__ __device__ constexpr int halo_px_cap(int RT, int CK) { return RT == 4 ?
 // consecutive slots), 176-B weight rows
 __host__ __device__ constexpr int halo_ld(int CK) { return CK == 8 ? 8 : CK + 8; }       // 48 / 80 B: odd # of 16-B slots
 __host__ __device__ constexpr int wrow_ld(int CK) { return CK == 8 ? 88 : 9 * CK + 8; }  // 304 / 592 B: odd # of 16-B slots
+// M16 weight rows: piece p of a tap stored at p ^ wswz(row) (see k_halo_conv)
+__device__ __forceinline__ int wswz(int row) { return ((row >> 2) & 1) * 2; }
 
 // Loader piece `item` -> (halo pixel, 16-B piece within the pixel). ds_write_b128 is banked per 8-lane
 // group over 8 slots ((a/4) mod 32): 8 lanes on 8 consecutive pixels at one piece land on 8 distinct
@@ -242,16 +244,21 @@ template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     constexpr int BN = 32 * NT;
     constexpr int PPX = CK / 8;                          // 16-B pieces per pixel (and per tap of a weight row)
-    // M16 (every CK = 32 instance): v_mfma_f32_16x16x32_bf16, one k-step per tap. Same LDS bytes and MFMA cycles per
-    // FLOP as 32x32x16 at the same wave tile, but the chip holds a higher clock under it (MI355X_MICROARCH.md, DVFS
-    // give-back item 7: 1.12-1.14x the FLOP/s with operands from LDS). Its fragments are 16 rows x 4 pieces, so the
-    // halo is stored piece-major ([piece][pixel], 16 B per pixel: 16 consecutive pixels of one ds_read_b128 lane group
-    // hit 16 distinct bank slots) and the weight rows take a 38-slot stride (= 2 mod 4: rows r at piece p and r' at
-    // p + 1 never share a slot within a lane group).
+    // M16 (every CK = 32 instance but the BNS dgrads): v_mfma_f32_16x16x32_bf16, one k-step per tap. Same LDS bytes and
+    // MFMA cycles per FLOP as 32x32x16 at the same wave tile, but the chip holds a higher clock under it
+    // (MI355X_MICROARCH.md, DVFS give-back item 7: 1.12-1.14x the FLOP/s with operands from LDS; measured here 3-6 %
+    // per layer). Its fragments are 16 rows x 4 pieces, so the halo is stored piece-major ([piece][pixel], 16 B per
+    // pixel: the 16 consecutive pixels of one ds_read_b128 lane group hit 16 distinct bank slots) and the weight rows
+    // (36 slots, unpadded) swap their pieces by row, piece ^ wswz(row): rows r (piece p) and r' (piece p + 1) of one lane
+    // group land on 16 distinct slots (the 4-row classes r mod 16 in {0-3, 12-15} / {4-11} map to slot residues
+    // {0,2} / {1,3} mod 4).
     // Not the BNS dgrads: their y prefetch and BatchNorm-backward constants beside the 16x16 fragment ring spill at
     // RT 4 (461 vs 236 us per launch); they are HBM-bound full-resolution layers, where the shape buys nothing.
+    // (Tried: 512-pixel items, NT = 2 x RT = 4 at 12x32 / 10x40 tiles with a 512-pixel halo, to halve the weight
+    // staging per MFMA: 10-30 % slower per layer. Those tiles hold 384-400 pixels, so a quarter of the MFMA columns
+    // idle, and the 128 accumulators leave no room for a fragment ring.)
     constexpr bool M16 = CK == 32 && IT == 1 && !BNS;
-    constexpr int HX_LD = halo_ld(CK), W_LD = M16 ? 9 * CK + 16 : wrow_ld(CK);
+    constexpr int HX_LD = halo_ld(CK), W_LD = M16 ? 9 * CK : wrow_ld(CK);
     constexpr int HPX = IT == 2 ? 384 : halo_px_cap(RT, CK);  // IT = 2: the CK = 32 tilings (halo <= 384 px)
     constexpr int HP = (HPX * PPX + 255) / 256;          // halo pieces per loader thread
     constexpr int WPIECES = BN * 9 * PPX;                // weight pieces per chunk
@@ -262,8 +269,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     static_assert(IT == 1 || (IT == 2 && HP * IT <= 16), "item masks fit 16 bits");
     constexpr int KS = (9 * CK + 15) / 16;               // 16-deep k-steps per chunk (CK 8: 5, the last half padding)
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
-    // epilogue transpose scratch: 32 pixels x BN channels per MFMA wave (its own region, no block sync)
-    __shared__ __attribute__((aligned(16))) __bf16 scr[4 * 32 * BN];
+    // epilogue transpose scratch: 32 (M16: 16) pixels x BN channels per MFMA wave (its own region, no block sync)
+    constexpr int SCR_PX = M16 ? 16 : 32;
+    __shared__ __attribute__((aligned(16))) __bf16 scr[4 * SCR_PX * BN];
 
     // waves 0-3 land on the 4 different SIMDs (dispatch order 0->2->1->3, measured), and so do 4-7:
     // one MFMA wave and one loader wave per SIMD
@@ -423,7 +431,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             for (int i = 0; i < W_PER_THREAD; ++i) {
                 const int item = ltid + i * 256;
                 const int co = item / (9 * PPX), r = item - co * (9 * PPX);
-                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * W_LD + r * 8) = wr[i];
+                const int rs = M16 ? r ^ wswz(co) : r;  // M16: pieces swapped by row (conflict-free 16x16 reads)
+                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * W_LD + rs * 8) = wr[i];
             }
         };
         auto load = [&](auto S) __attribute__((always_inline)) {  // halo of chunk (ld_item, ld_cc) -> register set S, then advance
@@ -618,7 +627,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const int k = i * ER + r;
             erel[k / 2] = (erel[k / 2] & ~(0xffffu << (16 * (k & 1)))) | (v << (16 * (k & 1)));
         }
-    __bf16* const scw = scr + wid * 32 * BN;
+    __bf16* const scw = scr + wid * SCR_PX * BN;
     // BNS: the lane's 8 channels are fixed (piece lane % PPP): their BatchNorm constants in registers, and the y
     // pieces of an item's stores prefetched while its last chunk is in the matrix core
     constexpr int NBK = BNS ? 8 : 1, NYQ = BNS ? RT * ER : 1;
@@ -731,7 +740,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #pragma unroll
                 for (int t = 0; t < 2 * NT; ++t)
                     a16[sl][t] = *reinterpret_cast<const bf16x8*>(wl + (t * 16 + (lane & 15)) * W_LD + tap * CK +
-                                                                  (lane >> 4) * 8);
+                                                                  ((lane >> 4) ^ wswz(lane & 15)) * 8);
 #pragma unroll
                 for (int i = 0; i < 2 * RT; ++i) b16[sl][i] = *reinterpret_cast<const bf16x8*>(hx + abase16[i] + toff);
             };
@@ -796,22 +805,23 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(split ? p.out1 + (size_t)b * hw_img * (p.N - ns) : p.out0), (short)0,
                 split ? hw_img * (p.N - ns) * 2 : 0, 0x00020000);
+            constexpr int NPART = M16 ? 2 * RT : RT;  // epilogue passes: 16-pixel halves (M16) or 32-pixel tiles
+            constexpr int RPP = M16 ? ER / 2 : ER;     // store instructions per pass
 #pragma unroll
-            for (int i = 0; i < RT; ++i) {
+            for (int i2 = 0; i2 < NPART; ++i2) {
+              const int i = M16 ? i2 >> 1 : i2;        // 32-pixel tile
+              const int r0 = M16 ? (i2 & 1) * RPP : 0;  // its first store row of this pass
               if constexpr (M16) {
-                // lane l holds channels 4 * (l >> 4) + 0..3 of each 16-channel block for pixel l & 15 of each half:
+                // lane l holds channels 4 * (l >> 4) + 0..3 of each 16-channel block for pixel l & 15 of the half:
                 // 8-B pieces into the pixel rows of the scratch (the read-back below takes whole 16-B pieces)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
+                for (int t = 0; t < 2 * NT; ++t) {
+                    bf16x4 v;
 #pragma unroll
-                    for (int t = 0; t < 2 * NT; ++t) {
-                        bf16x4 v;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[2 * i + h][t][q];
-                        const int px = h * 16 + (lane & 15), c = t * 16 + 4 * (lane >> 4);
-                        *reinterpret_cast<uint2*>(scw + px * BN + swz(c >> 3, px) * 8 + (c & 4)) =
-                            *reinterpret_cast<uint2*>(&v);
-                    }
+                    for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[i2][t][q];
+                    const int px = lane & 15, c = t * 16 + 4 * (lane >> 4);
+                    *reinterpret_cast<uint2*>(scw + px * BN + swz(c >> 3, px) * 8 + (c & 4)) = *reinterpret_cast<uint2*>(&v);
+                }
               } else {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
@@ -836,8 +846,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
               }
                 asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
 #pragma unroll
-                for (int r = 0; r < ER; ++r) {
-                    const int px = r * EPR + lane / PPP, j = lane % PPP;
+                for (int rr = 0; rr < RPP; ++rr) {
+                    const int r = r0 + rr;
+                    const int px = rr * EPR + lane / PPP, j = lane % PPP;  // pixel within the pass's scratch rows
                     const uint4 v = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
                     const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
                     const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
@@ -1839,7 +1850,8 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
     p.prio = halo_prio(a);
     p.dbg = g_wg_dbg;
-    SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= (t.it == 2 ? 384 : halo_px_cap(t.rt, t.ck)) && t.th * t.tw <= 128 * t.rt &&
+    const int cap = t.it == 2 ? 384 : halo_px_cap(t.rt, t.ck);
+    SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= cap && t.th * t.tw <= 128 * t.rt &&
                    t.th < 64 && t.tw < 512,
                "sd_conv_gemm(halo): tile %dx%d (RT %d, CK %d)", t.th, t.tw, t.rt, t.ck);
     SD_REQUIRE((long long)batch * p.tiles < (1LL << 30), "sd_conv_gemm(halo): too many tiles");

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(256) void k_heads_finalize(const float* __restrict_
 // 4 pixels per thread per iteration (one 32-bit mask word, one float4 of targets), block
 // reduction, one atomic per block
 __global__ __launch_bounds__(256) void k_count_valid(const float* __restrict__ t, const uint8_t* __restrict__ m,
-                                                     long long P, int* count) {
+                                                     long long P, int* count, int ncount) {
     int c = 0;
     const long long P4 = P / 4;
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < P4; i += (long long)gridDim.x * 256) {
@@ -355,18 +355,20 @@ __global__ __launch_bounds__(256) void k_count_valid(const float* __restrict__ t
     __syncthreads();
     if (threadIdx.x == 0) {
         const int s = red[0] + red[1] + red[2] + red[3];
-        if (s) atomicAdd(count, s);
+        if (s)
+            for (int k = 0; k < ncount; ++k) atomicAdd(count + k, s);
     }
 }
 
 __global__ __launch_bounds__(256) void k_count_valid_scalar(const float* __restrict__ t, const uint8_t* __restrict__ m,
-                                                            long long P, int* count) {
+                                                            long long P, int* count, int ncount) {
     int c = 0;
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < P; i += (long long)gridDim.x * 256)
         c += (m[i] != 0 && isfinite(t[i])) ? 1 : 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+    if ((threadIdx.x & 63) == 0 && c)
+        for (int k = 0; k < ncount; ++k) atomicAdd(count + k, c);
 }
 
 int heads_rows(long long P) {
@@ -409,19 +411,20 @@ int launch_heads(int C, int mode, const void* y, const float* sc, const float* s
 
 }  // namespace
 
-extern "C" int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, sd_stream s) {
-    SD_REQUIRE(target && mask && count && pixels > 0, "sd_count_valid: bad args");
-    if (hipMemsetAsync(count, 0, sizeof(int), to_stream(s)) != hipSuccess) return sd_check_launch("sd_count_valid");
+extern "C" int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount,
+                              sd_stream s) {
+    SD_REQUIRE(target && mask && count && pixels > 0 && ncount >= 1 && ncount <= 4, "sd_count_valid: bad args");
+    if (hipMemsetAsync(count, 0, sizeof(int) * ncount, to_stream(s)) != hipSuccess) return sd_check_launch("sd_count_valid");
     long long g = (pixels / 4 + 255) / 256;
     if (g > 1024) g = 1024;
     if (g < 1) g = 1;
     // the vector path needs a 4-B aligned mask and 16-B aligned targets; otherwise scalar-only
     const bool vec = ((uintptr_t)mask % 4 == 0) && ((uintptr_t)target % 16 == 0);
     hipLaunchKernelGGL(k_count_valid, dim3((int)g), dim3(256), 0, to_stream(s), target, mask,
-                       vec ? (long long)pixels : 0LL, count);
+                       vec ? (long long)pixels : 0LL, count, ncount);
     if (!vec)
         hipLaunchKernelGGL(k_count_valid_scalar, dim3((int)g), dim3(256), 0, to_stream(s), target, mask,
-                           (long long)pixels, count);
+                           (long long)pixels, count, ncount);
     return sd_check_launch("sd_count_valid");
 }
 

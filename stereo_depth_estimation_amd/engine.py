@@ -146,8 +146,9 @@ class UNetEngine:
         self.c1 = c[0]
         # persistent small device state
         dev = self.device
-        self.count = torch.zeros(1, dtype=torch.int32, device=dev)  # loss normaliser (global under DDP)
-        self.count_local = torch.zeros(1, dtype=torch.int32, device=dev)  # this rank's valid pixels
+        # [loss normaliser (global under DDP), this rank's valid pixels]: written together by sd_count_valid
+        self._counts = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.count, self.count_local = self._counts[0:1], self._counts[1:2]
         self.metrics = torch.zeros(5, dtype=torch.float64, device=dev)
         self.adam_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_scratch = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -539,9 +540,8 @@ class UNetEngine:
     def count_valid(self, target: torch.Tensor, valid: torch.Tensor):
         """train.py:329-330 valid count, on device: count_local (this rank's pixels, for the
         metric sums) and count (the loss normaliser; DDP all-reduces it to the global count)."""
-        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self.count_local.data_ptr(),
+        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts.data_ptr(), 2,
                self._s())
-        self.count.copy_(self.count_local)
 
     # ------------------------------------------------------------------ backward
     @staticmethod

@@ -3,6 +3,7 @@ FoundationStereo-layout tree of PNG pairs and its reference-format `.npz` cache,
 `FoundationStereoDataset` + `DeviceLoader` (worker processes -> pinned uint8 -> side-stream H2D -> HIP decode /
 resize / augment), alone and feeding `run_epoch` training. Compare with bench.py's HBM-resident `value`.
     python tools/loader_bench.py [pairs] [H] [W] [batch]
+    python tools/loader_bench.py c4 [pairs] [H] [W] [batch]     (BASELINE config 4 per GPU: 640x480, 16 pairs)
 Prints one JSON line. Data: random smooth images (no dataset on the box)."""
 
 import json
@@ -106,7 +107,64 @@ def host_loader_rate(ds, batch, workers, epochs=2):
     return n / (time.perf_counter() - t0)
 
 
+def resident_rate(batch, H, W, steps=30):
+    """bench.py's HBM-resident rate for the same config (a ring of 4 pre-generated device batches)."""
+    from stereo_depth_estimation_amd.data import synthetic_batch
+    from stereo_depth_estimation_amd.train import train_step
+
+    torch.manual_seed(42)
+    model = StereoUNet(precision="bf16").cuda()
+    opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    ring = [synthetic_batch(batch, H, W, seed=i, device="cuda") for i in range(4)]
+    for i in range(5):
+        b = ring[i % 4]
+        train_step(model, opt, b["input"], b["target"], b["valid_mask"])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        b = ring[i % 4]
+        train_step(model, opt, b["input"], b["target"], b["valid_mask"])
+    torch.cuda.synchronize()
+    return steps * batch / (time.perf_counter() - t0)
+
+
+def c4(pairs=256, H=480, W=640, batch=16):
+    """BASELINE config 4 per GPU (640x480, 16 pairs, async augmentation with pinned H2D overlap): loader-fed training as a
+    fraction of the HBM-resident rate, for the reference-format cache (+ augmentation) and PNG (+ augmentation) sources."""
+    out = {"config": "C4 per GPU: 640x480, batch 16, bf16", "pairs": pairs, "hw": [H, W], "batch": batch}
+    out["resident_pairs_s"] = round(resident_rate(batch, H, W), 1)
+    print(f"resident: {out}", file=sys.stderr, flush=True)
+    aug = dict(augment=True, brightness_jitter=0.2, contrast_jitter=0.2, saturation_jitter=0.2, hue_jitter=0.05,
+               gamma_jitter=0.1, noise_std_max=0.02, blur_prob=0.3, blur_sigma_max=1.0)
+    with tempfile.TemporaryDirectory(dir="/tmp") as tmp:
+        root, cache = Path(tmp) / "data", Path(tmp) / "cache"
+        t0 = time.perf_counter()
+        write_tree(root, pairs, H, W)
+        samples = D.discover_samples(root)
+        png = D.FoundationStereoDataset(samples, image_size=(H, W), cache_root=cache)
+        for _ in D.DeviceLoader(png, batch, num_workers=8, device="cuda"):
+            pass
+        torch.cuda.synchronize()
+        out["tree_and_cache_write_s"] = round(time.perf_counter() - t0, 1)
+        print(f"tree + cache: {out}", file=sys.stderr, flush=True)
+        arms = {"cache_aug_native": (D.FoundationStereoDataset(samples, image_size=(H, W), cache_root=cache,
+                                                               require_cache=True, **aug), 0, True),
+                "cache_native": (D.FoundationStereoDataset(samples, image_size=(H, W), cache_root=cache,
+                                                           require_cache=True), 0, True),
+                "png_aug_native": (D.FoundationStereoDataset(samples, image_size=(H, W), **aug), 0, True),
+                "png_aug_w16": (D.FoundationStereoDataset(samples, image_size=(H, W), **aug), 16, False)}
+        for name, (ds, workers, native) in arms.items():
+            r = train_rate(ds, batch, workers, native=native, epochs=3)
+            out[f"train_{name}_pairs_s"] = round(r, 1)
+            out[f"train_{name}_frac_of_resident"] = round(r / out["resident_pairs_s"], 3)
+            print(f"{name}: {out}", file=sys.stderr, flush=True)
+    print(json.dumps(out), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "c4":
+        c4(*(int(a) for a in sys.argv[2:]))
+        return
     pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     H = int(sys.argv[2]) if len(sys.argv) > 2 else 240
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 320
