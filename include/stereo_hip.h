@@ -301,7 +301,7 @@ int sd_stereo_from_cache(const uint8_t* left, const uint8_t* right, const uint16
  * functional ops), in place on input [B][6][H][W] f32 = 2B RGB images (left, right of each pair).
  * params [2B][7] f32 per image: brightness, contrast, saturation factors, hue shift, gamma, blur sigma
  * (0 = no blur), noise std. blur_ksize odd in [3, 31]. Noise: counter-based N(0,1) keyed by `seed`.
- * work: scratch of B*6*H*W + 2B floats. */
+ * work: 8-B aligned scratch of B*6*H*W + 128*B floats (the images, then 64 fp64 contrast partial sums per pair). */
 int sd_augment_rgb(float* input, int batch, int H, int W, const float* params, int blur_ksize, uint64_t seed,
                    float* work, sd_stream s);
 

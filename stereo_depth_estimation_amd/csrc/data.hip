@@ -72,6 +72,38 @@ __global__ void k_stereo_from_cache(const uint8_t* __restrict__ left, const uint
     }
 }
 
+// 4 pixels per thread (plane % 4 == 0): three 4-B loads per image of the packed HWC bytes, one 8-B load of the f16
+// disparities, 16-B stores per output plane (the per-pixel form issued 6 byte loads and 8 scalar stores per pixel)
+__global__ void k_stereo_from_cache4(const uint8_t* __restrict__ left, const uint8_t* __restrict__ right,
+                                     const __half* __restrict__ disp, int B, int Ho, int Wo, float* __restrict__ input,
+                                     float* __restrict__ target, uint8_t* __restrict__ valid) {
+    const long long plane = (long long)Ho * Wo, total4 = (long long)B * plane / 4;
+    for (long long q = blockIdx.x * 256LL + threadIdx.x; q < total4; q += (long long)gridDim.x * 256) {
+        const long long e = q * 4;
+        const int b = (int)(e / plane);
+        const int rem = (int)(e - (long long)b * plane);
+        float* in_b = input + (size_t)b * 6 * plane + rem;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>((side ? right : left) + (size_t)e * 3);
+            const uint32_t w0 = src[0], w1 = src[1], w2 = src[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+            const uint8_t v[12] = {(uint8_t)w0, (uint8_t)(w0 >> 8), (uint8_t)(w0 >> 16), (uint8_t)(w0 >> 24),
+                                   (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24),
+                                   (uint8_t)w2, (uint8_t)(w2 >> 8), (uint8_t)(w2 >> 16), (uint8_t)(w2 >> 24)};
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                *reinterpret_cast<float4*>(in_b + (3 * side + c) * plane) =
+                    make_float4((float)v[c] / 255.f, (float)v[3 + c] / 255.f, (float)v[6 + c] / 255.f, (float)v[9 + c] / 255.f);
+        }
+        const uint2 dh = *reinterpret_cast<const uint2*>(disp + e);
+        const __half* h = reinterpret_cast<const __half*>(&dh);
+        const float t0 = __half2float(h[0]), t1 = __half2float(h[1]), t2 = __half2float(h[2]), t3 = __half2float(h[3]);
+        *reinterpret_cast<float4*>(target + e) = make_float4(t0, t1, t2, t3);
+        *reinterpret_cast<uint32_t*>(valid + e) =
+            (uint32_t)(t0 > 0.f) | (uint32_t)(t1 > 0.f) << 8 | (uint32_t)(t2 > 0.f) << 16 | (uint32_t)(t3 > 0.f) << 24;
+    }
+}
+
 int grid_for(long long work) {
     long long g = (work + 255) / 256;
     if (g > 16384) g = 16384;
@@ -96,8 +128,16 @@ extern "C" int sd_stereo_from_cache(const uint8_t* left, const uint8_t* right, c
                                     int Ho, int Wo, float* input, float* target, uint8_t* valid, sd_stream s) {
     SD_REQUIRE(left && right && disp_f16 && input && target && valid, "sd_stereo_from_cache: null pointer");
     SD_REQUIRE(batch > 0 && Ho > 0 && Wo > 0, "sd_stereo_from_cache: bad sizes");
-    hipLaunchKernelGGL(k_stereo_from_cache, dim3(grid_for((long long)batch * Ho * Wo)), dim3(256), 0, to_stream(s),
-                       left, right, reinterpret_cast<const __half*>(disp_f16), batch, Ho, Wo, input, target, valid);
+    const bool vec = ((long long)Ho * Wo) % 4 == 0 && (uintptr_t)left % 4 == 0 && (uintptr_t)right % 4 == 0 &&
+                     (uintptr_t)disp_f16 % 8 == 0 && (uintptr_t)input % 16 == 0 && (uintptr_t)target % 16 == 0 &&
+                     (uintptr_t)valid % 4 == 0;
+    if (vec)
+        hipLaunchKernelGGL(k_stereo_from_cache4, dim3(grid_for((long long)batch * Ho * Wo / 4)), dim3(256), 0,
+                           to_stream(s), left, right, reinterpret_cast<const __half*>(disp_f16), batch, Ho, Wo, input,
+                           target, valid);
+    else
+        hipLaunchKernelGGL(k_stereo_from_cache, dim3(grid_for((long long)batch * Ho * Wo)), dim3(256), 0, to_stream(s),
+                           left, right, reinterpret_cast<const __half*>(disp_f16), batch, Ho, Wo, input, target, valid);
     return sd_check_launch("sd_stereo_from_cache");
 }
 
@@ -120,14 +160,16 @@ __device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.f), 
 __device__ __forceinline__ float blend(float a, float b, float r) { return clamp01(r * a + (1.f - r) * b); }
 __device__ __forceinline__ float gray(float r, float g, float b) { return 0.2989f * r + 0.587f * g + 0.114f * b; }
 
-// per-image mean of gray(brightness-adjusted image) (adjust_contrast's mean), fp64 accumulation
+// per-image mean of gray(brightness-adjusted image) (adjust_contrast's mean), fp64 accumulation: MEAN_SPLIT blocks
+// per image each write one partial sum (an image is 0.3 M pixels at 640x480: one block per image took ~60 us)
+constexpr int MEAN_SPLIT = 32;
 __global__ void k_aug_gray_mean(const float* __restrict__ input, int HW, const float* __restrict__ params,
-                                float* __restrict__ mean) {
-    const int im = blockIdx.x;  // image = 2*pair + side
+                                double* __restrict__ partial) {
+    const int im = blockIdx.y;  // image = 2*pair + side
     const float* x = input + ((size_t)(im >> 1) * 6 + (im & 1) * 3) * HW;
     const float fb = params[im * AUG_P + 0];
     double acc = 0.0;
-    for (int i = threadIdx.x; i < HW; i += 256)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < HW; i += MEAN_SPLIT * 256)
         acc += gray(clamp01(fb * x[i]), clamp01(fb * x[HW + i]), clamp01(fb * x[2 * HW + i]));
     __shared__ double red[256];
     red[threadIdx.x] = acc;
@@ -136,7 +178,7 @@ __global__ void k_aug_gray_mean(const float* __restrict__ input, int HW, const f
         if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) mean[im] = (float)(red[0] / HW);
+    if (threadIdx.x == 0) partial[im * MEAN_SPLIT + blockIdx.x] = red[0];
 }
 
 __device__ __forceinline__ void hue_shift(float& r, float& g, float& b, float shift) {
@@ -180,83 +222,113 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
     x ^= x >> 33;
     return (uint32_t)x;
 }
-__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t idx) {  // Box-Muller on two hashed uniforms
+// Box-Muller on two hashed uniforms: the pair of independent N(0,1) values (r cos, r sin) of counter idx
+__device__ __forceinline__ float2 normal2_at(uint64_t seed, uint64_t idx) {
     const float u1 = ((mix32(seed ^ (idx * 2 + 1) * 0x9E3779B97F4A7C15ULL) >> 8) + 1) * (1.f / 16777217.f);
     const float u2 = (mix32(seed + (idx * 2 + 2) * 0xD1B54A32D192ED03ULL) >> 8) * (1.f / 16777216.f);
-    return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+    const float r = sqrtf(-2.f * logf(u1));
+    float sn, cs;
+    sincospif(2.f * u2, &sn, &cs);
+    return make_float2(r * cs, r * sn);
+}
+// x^g for x in [0, 1] (torchvision adjust_gamma, gain 1): exp2(g log2 x) on the hardware transcendentals (~1 ulp each;
+// powf's exact-rounding path cost most of the pointwise kernel's time); 0^g = 0 for g > 0
+__device__ __forceinline__ float pow01(float x, float g) {
+    return x > 0.f ? __builtin_amdgcn_exp2f(g * __builtin_amdgcn_logf(x)) : (g == 0.f ? 1.f : 0.f);
 }
 
-// brightness, contrast, saturation, hue, gamma -> work (same layout as input)
-__global__ void k_aug_pointwise(const float* __restrict__ input, int B, int HW, const float* __restrict__ params,
-                                const float* __restrict__ mean, float* __restrict__ work) {
-    const long long total = (long long)2 * B * HW;
-    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const int im = (int)(e / HW), px = (int)(e - (long long)im * HW);
-        const size_t base = ((size_t)(im >> 1) * 6 + (im & 1) * 3) * HW + px;
-        const float* pr = params + im * AUG_P;
+// brightness, contrast, saturation, hue, gamma -> work (same layout as input); blockIdx.y = image, whose contrast mean
+// the block sums from the partials once
+__global__ void k_aug_pointwise(const float* __restrict__ input, int HW, const float* __restrict__ params,
+                                const double* __restrict__ partial, float* __restrict__ work) {
+    const int im = blockIdx.y;
+    __shared__ float s_m;
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < MEAN_SPLIT; ++k) t += partial[im * MEAN_SPLIT + k];
+        s_m = (float)(t / HW);
+    }
+    __syncthreads();
+    const float m = s_m;
+    const float* pr = params + im * AUG_P;
+    const float fb = pr[0], fc = pr[1], fs = pr[2], fh = pr[3], fg = pr[4];
+    const size_t base0 = ((size_t)(im >> 1) * 6 + (im & 1) * 3) * HW;
+    for (int px = blockIdx.x * 256 + threadIdx.x; px < HW; px += gridDim.x * 256) {
+        const size_t base = base0 + px;
         float r = input[base], g = input[base + HW], b = input[base + 2 * HW];
-        r = clamp01(pr[0] * r);  // brightness: blend with zeros
-        g = clamp01(pr[0] * g);
-        b = clamp01(pr[0] * b);
-        const float m = mean[im];  // contrast
-        r = blend(r, m, pr[1]);
-        g = blend(g, m, pr[1]);
-        b = blend(b, m, pr[1]);
+        r = clamp01(fb * r);  // brightness: blend with zeros
+        g = clamp01(fb * g);
+        b = clamp01(fb * b);
+        r = blend(r, m, fc);  // contrast
+        g = blend(g, m, fc);
+        b = blend(b, m, fc);
         const float l = gray(r, g, b);  // saturation
-        r = blend(r, l, pr[2]);
-        g = blend(g, l, pr[2]);
-        b = blend(b, l, pr[2]);
-        hue_shift(r, g, b, pr[3]);  // the reference calls adjust_hue even for a zero shift
-        r = clamp01(powf(r, pr[4]));  // gamma (gain 1)
-        g = clamp01(powf(g, pr[4]));
-        b = clamp01(powf(b, pr[4]));
+        r = blend(r, l, fs);
+        g = blend(g, l, fs);
+        b = blend(b, l, fs);
+        hue_shift(r, g, b, fh);  // the reference calls adjust_hue even for a zero shift
+        r = clamp01(pow01(r, fg));  // gamma (gain 1)
+        g = clamp01(pow01(g, fg));
+        b = clamp01(pow01(b, fg));
         work[base] = r;
         work[base + HW] = g;
         work[base + 2 * HW] = b;
     }
 }
 
-// optional gaussian blur (per-image sigma, 0 = off), + noise, clamp -> input
-__global__ void k_aug_blur_noise(const float* __restrict__ work, int B, int H, int W, const float* __restrict__ params,
-                                 int ks, uint64_t seed, float* __restrict__ input) {
+// optional gaussian blur (per-image sigma, 0 = off), + noise, clamp -> input; blockIdx.y = plane (image, channel), whose
+// normalised 1-D kernel the block builds once in LDS (_get_gaussian_kernel1d: linspace(-(k-1)/2, (k-1)/2, k),
+// exp(-0.5 (x/sigma)^2), normalised)
+__global__ void k_aug_blur_noise(const float* __restrict__ work, int H, int W, const float* __restrict__ params, int ks,
+                                 uint64_t seed, float* __restrict__ input) {
     const int HW = H * W;
-    const long long total = (long long)2 * B * 3 * HW;
     const int half = ks / 2;
-    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const int plane = (int)(e / HW), px = (int)(e - (long long)plane * HW);
-        const int im = plane / 3, c = plane - im * 3;
-        const size_t base = ((size_t)(im >> 1) * 6 + (im & 1) * 3 + c) * HW;
-        const float* pr = params + im * AUG_P;
-        const float sigma = pr[5];
-        float v;
-        if (sigma > 0.f) {
-            // _get_gaussian_kernel1d: linspace(-(k-1)/2, (k-1)/2, k), exp(-0.5 (x/sigma)^2), normalised
-            float k1[31];
-            float ksum = 0.f;
-            for (int i = 0; i < ks; ++i) {
-                const float x = (float)(i - half) / sigma;
-                k1[i] = expf(-0.5f * x * x);
-                ksum += k1[i];
-            }
-            for (int i = 0; i < ks; ++i) k1[i] /= ksum;
-            const int y = px / W, x = px - y * W;
-            float acc = 0.f;
-            for (int i = 0; i < ks; ++i) {
-                int yy = y + i - half;
-                yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);  // reflect
-                for (int j = 0; j < ks; ++j) {
-                    int xx = x + j - half;
-                    xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
-                    acc += (k1[i] * k1[j]) * work[base + (size_t)yy * W + xx];
-                }
-            }
-            v = acc;
-        } else {
-            v = work[base + px];
+    const int plane = blockIdx.y, im = plane / 3, c = plane - im * 3;
+    const size_t base = ((size_t)(im >> 1) * 6 + (im & 1) * 3 + c) * HW;
+    const float* pr = params + im * AUG_P;
+    const float sigma = pr[5], std = pr[6];
+    __shared__ float k1[31];
+    if (threadIdx.x == 0 && sigma > 0.f) {
+        float ksum = 0.f;
+        for (int i = 0; i < ks; ++i) {
+            const float x = (float)(i - half) / sigma;
+            k1[i] = expf(-0.5f * x * x);
+            ksum += k1[i];
         }
-        const float std = pr[6];
-        if (std > 0.f) v += normal_at(seed, (uint64_t)e) * std;
-        input[base + px] = clamp01(v);
+        for (int i = 0; i < ks; ++i) k1[i] /= ksum;
+    }
+    __syncthreads();
+    // two adjacent pixels per thread, one Box-Muller draw for both
+    for (int px = 2 * (blockIdx.x * 256 + threadIdx.x); px < HW; px += 2 * gridDim.x * 256) {
+        float v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = px + h < HW ? px + h : px;  // odd HW: the last thread's second pixel repeats its first
+            if (sigma > 0.f) {
+                const int y = q / W, x = q - y * W;
+                float acc = 0.f;
+                for (int i = 0; i < ks; ++i) {
+                    int yy = y + i - half;
+                    yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);  // reflect
+                    const float* row = work + base + (size_t)yy * W;
+                    for (int j = 0; j < ks; ++j) {
+                        int xx = x + j - half;
+                        xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+                        acc += (k1[i] * k1[j]) * row[xx];
+                    }
+                }
+                v[h] = acc;
+            } else {
+                v[h] = work[base + q];
+            }
+        }
+        if (std > 0.f) {
+            const float2 z = normal2_at(seed, ((uint64_t)plane * HW + px) >> 1);
+            v[0] += z.x * std;
+            v[1] += z.y * std;
+        }
+        input[base + px] = clamp01(v[0]);
+        if (px + 1 < HW) input[base + px + 1] = clamp01(v[1]);
     }
 }
 
@@ -264,16 +336,18 @@ __global__ void k_aug_blur_noise(const float* __restrict__ work, int B, int H, i
 
 extern "C" int sd_augment_rgb(float* input, int batch, int H, int W, const float* params, int blur_ksize,
                               uint64_t seed, float* work, sd_stream s) {
-    SD_REQUIRE(input && params && work && batch > 0 && H > 0 && W > 0, "sd_augment_rgb: bad args");
+    SD_REQUIRE(input && params && work && batch > 0 && H > 0 && W > 0 && ((uintptr_t)work % 8) == 0,
+               "sd_augment_rgb: bad args");
     SD_REQUIRE(blur_ksize >= 3 && blur_ksize % 2 == 1 && blur_ksize <= 31, "sd_augment_rgb: blur_ksize %d", blur_ksize);
     SD_REQUIRE(blur_ksize / 2 < H && blur_ksize / 2 < W, "sd_augment_rgb: blur kernel larger than the image");
     const int HW = H * W;
-    float* mean = work + (size_t)batch * 6 * HW;
+    // the contrast partial sums (2*batch*MEAN_SPLIT doubles) follow the images in `work` (8-B aligned: 6*HW*batch is even)
+    double* partial = reinterpret_cast<double*>(work + (size_t)batch * 6 * HW);
     hipStream_t st = to_stream(s);
-    hipLaunchKernelGGL(k_aug_gray_mean, dim3(2 * batch), dim3(256), 0, st, input, HW, params, mean);
-    hipLaunchKernelGGL(k_aug_pointwise, dim3(grid_for(2LL * batch * HW)), dim3(256), 0, st, input, batch, HW, params,
-                       mean, work);
-    hipLaunchKernelGGL(k_aug_blur_noise, dim3(grid_for(6LL * batch * HW)), dim3(256), 0, st, work, batch, H, W, params,
-                       blur_ksize, seed, input);
+    const int per = (HW + 255) / 256;
+    const int gx = per < 64 ? per : 64;  // blocks per image / plane (2*batch or 6*batch rows of the grid)
+    hipLaunchKernelGGL(k_aug_gray_mean, dim3(MEAN_SPLIT, 2 * batch), dim3(256), 0, st, input, HW, params, partial);
+    hipLaunchKernelGGL(k_aug_pointwise, dim3(gx, 2 * batch), dim3(256), 0, st, input, HW, params, partial, work);
+    hipLaunchKernelGGL(k_aug_blur_noise, dim3(gx, 6 * batch), dim3(256), 0, st, work, H, W, params, blur_ksize, seed, input);
     return sd_check_launch("sd_augment_rgb");
 }

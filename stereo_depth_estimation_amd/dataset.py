@@ -327,10 +327,10 @@ class DeviceLoader:
     """Iterates device batch dicts ``{"input","target","valid_mask"}`` for ``run_epoch``.
 
     Wraps a ``torch.utils.data.DataLoader`` over a :class:`FoundationStereoDataset` (uint8
-    collate, pinned memory, the reference's worker options). Each host batch is copied on a
-    side HIP stream and turned into the reference's tensors there by the HIP kernels; the
-    consumer's stream waits on an event, so copy and preparation of batch i+1 overlap training
-    on batch i.
+    collate, pinned memory, the reference's worker options). Each host batch is copied to the
+    device on a side HIP stream (DMA engines) and turned into the reference's tensors there by the
+    HIP kernels, beside the training step of the batch before it; the consumer's stream waits on
+    an event.
     """
 
     def __init__(self, dataset: FoundationStereoDataset, batch_size: int, shuffle: bool = False, num_workers: int = 0,
@@ -359,24 +359,57 @@ class DeviceLoader:
         self._stream = None
         self._batches = 0
         self._seed_drawn = False
+        # the decode / augment kernels on the side stream beside the previous step (default), or on the consumer's
+        # stream right before the step (SD_LOADER_PREP_SIDE=0): 640x480 B=16 loader-fed training 1634 vs 1615 pairs/s
+        self._prep_side = os.environ.get("SD_LOADER_PREP_SIDE", "1") == "1"
 
     def __len__(self) -> int:
         return len(self.loader)
 
-    def _prepare(self, groups: list[dict]) -> dict:
-        L.load()
-        H, W = self.dataset.image_size
-        B = sum(len(g["index"]) for g in groups)
+    def _upload(self, groups: list[dict]) -> list[dict]:
+        """Side stream: the pinned uint8 frames (and augmentation factors) of a host batch to the device. The copies run
+        on the DMA engines; the seeds of the augmentation noise are drawn here, in batch order."""
         dev = self.device
+        staged = []
+        for g in groups:
+            n = len(g["index"])
+            st = {"g": g, "left": _pin(g["left"]).to(dev, non_blocking=True),
+                  "right": _pin(g["right"]).to(dev, non_blocking=True),
+                  "disparity": _pin(g["disparity"]).to(dev, non_blocking=True)}
+            if "aug" in g:
+                st["params"] = _pin(g["aug"].reshape(n * 2, AUG_PARAMS).contiguous()).to(dev, non_blocking=True)
+                st["seed"] = int(torch.randint(0, 2**62, (1,)).item())
+            staged.append(st)
+        return staged
+
+    def _finish(self, staged, ev, consumer) -> dict:
+        if isinstance(staged, dict):  # prepared on the side stream (SD_LOADER_PREP_SIDE=1)
+            consumer.wait_event(ev)
+            for t in staged.values():
+                t.record_stream(consumer)
+            return staged
+        return self._kernels(staged, ev, consumer)
+
+    def _kernels(self, staged: list[dict], ev, consumer) -> dict:
+        """Decode / resize / augment the uploaded uint8 frames into the reference's tensors on stream `consumer` (the
+        side stream by default, after the copies; ev = None) or on the training stream after the copy event."""
+        L.load()
+        if ev is not None:
+            consumer.wait_event(ev)
+        H, W = self.dataset.image_size
+        B = sum(len(st["g"]["index"]) for st in staged)
+        dev = self.device
+        s = L.stream_handle(dev)
         inp = torch.empty(B, 6, H, W, device=dev)
         tgt = torch.empty(B, 1, H, W, device=dev)
         val = torch.empty(B, 1, H, W, device=dev, dtype=torch.bool)
-        s = L.stream_handle(dev)
-        for g in groups:
+        for st in staged:
+            g = st["g"]
+            for k in ("left", "right", "disparity", "params"):
+                if k in st:
+                    st[k].record_stream(consumer)
+            left, right, disp = st["left"], st["right"], st["disparity"]
             n = len(g["index"])
-            left = _pin(g["left"]).to(dev, non_blocking=True)
-            right = _pin(g["right"]).to(dev, non_blocking=True)
-            disp = _pin(g["disparity"]).to(dev, non_blocking=True)
             contiguous = bool((g["index"] == torch.arange(g["index"][0], g["index"][0] + n)).all())
             gi = inp[g["index"][0]:g["index"][0] + n] if contiguous else torch.empty(n, 6, H, W, device=dev)
             gt = tgt[g["index"][0]:g["index"][0] + n] if contiguous else torch.empty(n, 1, H, W, device=dev)
@@ -395,12 +428,10 @@ class DeviceLoader:
                 for k, f in enumerate(g["cache_file"]):
                     if f:
                         save_cached_sample(Path(f), gi_h[k, :3], gi_h[k, 3:], gt_h[k])
-            if "aug" in g:
-                params = _pin(g["aug"].reshape(n * 2, AUG_PARAMS).contiguous()).to(dev, non_blocking=True)
-                work = torch.empty(n * 6 * H * W + 2 * n, device=dev)
-                seed = int(torch.randint(0, 2**62, (1,)).item())
-                L.call("sd_augment_rgb", gi.data_ptr(), n, H, W, params.data_ptr(), self.dataset.blur_kernel_size, seed,
-                       work.data_ptr(), s)
+            if "params" in st:
+                work = torch.empty(n * 6 * H * W + 128 * n, device=dev)
+                L.call("sd_augment_rgb", gi.data_ptr(), n, H, W, st["params"].data_ptr(), self.dataset.blur_kernel_size,
+                       st["seed"], work.data_ptr(), s)
             if not contiguous:
                 inp[g["index"].to(dev)] = gi
                 tgt[g["index"].to(dev)] = gt
@@ -497,7 +528,7 @@ class DeviceLoader:
                 if self.dataset.augment:
                     # drawn here, as batch k is handed over, so the main-process RNG sees the order of a
                     # num_workers=0 DataLoader: factors of batch k (per item in batch order, in __getitem__'s calls),
-                    # then the noise seeds _prepare draws for batch k's groups, then batch k+1's factors
+                    # then the noise seeds _upload draws for batch k's groups, then batch k+1's factors
                     ds = self.dataset
                     n = sum(len(g["index"]) for g in gs)
                     aug = np.stack([np.stack([ds.sample_augment_params(), ds.sample_augment_params()]) for _ in range(n)])
@@ -515,20 +546,15 @@ class DeviceLoader:
         for groups in (self._native_groups() if self.native else self.loader):
             self._stream.wait_stream(consumer)  # reuse of freed buffers is ordered after their last use
             with torch.cuda.stream(self._stream):
-                batch = self._prepare(groups)
+                staged = self._upload(groups)
+                if self._prep_side:  # A/B: the kernels beside the step instead of before it
+                    staged = self._kernels(staged, None, self._stream)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
             if self.native:
                 self._h2d_done[self._slot] = ev  # the pinned set may be refilled once its copies are done
             if pending is not None:
-                yield self._hand_over(*pending, consumer)
-            pending = (batch, ev)
+                yield self._finish(*pending, consumer)
+            pending = (staged, ev)
         if pending is not None:
-            yield self._hand_over(*pending, consumer)
-
-    @staticmethod
-    def _hand_over(batch, ev, consumer):
-        consumer.wait_event(ev)
-        for t in batch.values():
-            t.record_stream(consumer)
-        return batch
+            yield self._finish(*pending, consumer)

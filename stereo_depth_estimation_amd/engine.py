@@ -146,9 +146,10 @@ class UNetEngine:
         self.c1 = c[0]
         # persistent small device state
         dev = self.device
-        # [loss normaliser (global under DDP), this rank's valid pixels]: written together by sd_count_valid
-        self._counts = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.count, self.count_local = self._counts[0:1], self._counts[1:2]
+        # this rank's valid pixels (sd_count_valid) and the loss normaliser: the same tensor single-process; DDP gives
+        # `count` a tensor of its own, filled from count_local and all-reduced to the global count (ddp.DataParallel)
+        self.count_local = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.count = self.count_local
         self.metrics = torch.zeros(5, dtype=torch.float64, device=dev)
         self.adam_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_scratch = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -540,7 +541,7 @@ class UNetEngine:
     def count_valid(self, target: torch.Tensor, valid: torch.Tensor):
         """train.py:329-330 valid count, on device: count_local (this rank's pixels, for the
         metric sums) and count (the loss normaliser; DDP all-reduces it to the global count)."""
-        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts.data_ptr(), 2,
+        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self.count_local.data_ptr(), 1,
                self._s())
 
     # ------------------------------------------------------------------ backward

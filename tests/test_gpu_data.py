@@ -108,7 +108,7 @@ def _augment(lib, x, params, ks, seed=1):
     B, _, H, W = x.shape
     xd = x.clone().to(DEV)
     pd = torch.tensor(params, dtype=torch.float32).reshape(2 * B, 7).to(DEV)
-    work = torch.empty(B * 6 * H * W + 2 * B, device=DEV)
+    work = torch.empty(B * 6 * H * W + 128 * B, device=DEV)
     lib.call("sd_augment_rgb", xd.data_ptr(), B, H, W, pd.data_ptr(), ks, seed, work.data_ptr(), lib.stream_handle())
     torch.cuda.synchronize()
     return xd.cpu()

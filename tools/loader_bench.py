@@ -7,6 +7,7 @@ resize / augment), alone and feeding `run_epoch` training. Compare with bench.py
 Prints one JSON line. Data: random smooth images (no dataset on the box)."""
 
 import json
+import os
 import sys
 import tempfile
 import time
@@ -55,12 +56,12 @@ def loader_rate(ds, batch, workers, epochs=2, native=False):
     return n / (time.perf_counter() - t0)
 
 
-def train_rate(ds, batch, workers, epochs=2, native=False):
+def train_rate(ds, batch, workers, epochs=2, native=False, read_threads=16):
     torch.manual_seed(42)
     model = StereoUNet(precision="bf16").cuda()
     opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
     loader = D.DeviceLoader(ds, batch, shuffle=True, num_workers=workers, device="cuda", persistent_workers=True,
-                            drop_last=True, native=native)
+                            drop_last=True, native=native, read_threads=read_threads)
     run_epoch(model, loader, torch.device("cuda"), optimizer=opt)  # warm-up epoch
     torch.cuda.synchronize()
     t0, n = time.perf_counter(), 0
@@ -128,7 +129,7 @@ def resident_rate(batch, H, W, steps=30):
     return steps * batch / (time.perf_counter() - t0)
 
 
-def c4(pairs=256, H=480, W=640, batch=16):
+def c4(pairs=256, H=480, W=640, batch=16, epoch_pairs=2048):
     """BASELINE config 4 per GPU (640x480, 16 pairs, async augmentation with pinned H2D overlap): loader-fed training as a
     fraction of the HBM-resident rate, for the reference-format cache (+ augmentation) and PNG (+ augmentation) sources."""
     out = {"config": "C4 per GPU: 640x480, batch 16, bf16", "pairs": pairs, "hw": [H, W], "batch": batch}
@@ -146,6 +147,11 @@ def c4(pairs=256, H=480, W=640, batch=16):
             pass
         torch.cuda.synchronize()
         out["tree_and_cache_write_s"] = round(time.perf_counter() - t0, 1)
+        # epochs of `epoch_pairs` (the files repeated): a training epoch runs thousands of steps, so the per-epoch start
+        # (first batch read and copied with nothing to overlap, the end-of-epoch metric read) must not weigh more than it
+        # does there
+        samples = samples * max(1, epoch_pairs // len(samples))
+        out["epoch_pairs"] = len(samples)
         print(f"tree + cache: {out}", file=sys.stderr, flush=True)
         arms = {"cache_aug_native": (D.FoundationStereoDataset(samples, image_size=(H, W), cache_root=cache,
                                                                require_cache=True, **aug), 0, True),
@@ -153,8 +159,33 @@ def c4(pairs=256, H=480, W=640, batch=16):
                                                            require_cache=True), 0, True),
                 "png_aug_native": (D.FoundationStereoDataset(samples, image_size=(H, W), **aug), 0, True),
                 "png_aug_w16": (D.FoundationStereoDataset(samples, image_size=(H, W), **aug), 16, False)}
+        if os.environ.get("SD_C4_TRACE"):  # one arm only, for a kernel / memory-copy trace of loader-fed training
+            arm = os.environ["SD_C4_TRACE"]
+            ds, workers, native = arms[arm]
+            out[f"train_{arm}_pairs_s"] = round(train_rate(ds, batch, workers, native=native, epochs=2), 1)
+            print(json.dumps(out), flush=True)
+            return
+        if os.environ.get("SD_C4_SIDE_AB"):  # prep kernels before the step (default) vs beside it, alternating
+            ds = arms["cache_aug_native"][0]
+            for rnd in range(2):
+                for side in ("0", "1"):
+                    os.environ["SD_LOADER_PREP_SIDE"] = side
+                    out[f"ab_side{side}_r{rnd}_pairs_s"] = round(train_rate(ds, batch, 0, native=True, epochs=2), 1)
+            os.environ["SD_LOADER_PREP_SIDE"] = "0"
+            print(json.dumps(out), flush=True)
+            return
+        if os.environ.get("SD_C4_EXPERIMENTS"):  # where the cache+aug arm loses time (A/B arms, one process)
+            ds = arms["cache_aug_native"][0]
+            out["loader_only_cache_aug_native_pairs_s"] = round(loader_rate(ds, batch, 0, native=True), 1)
+            for rt in (4, 8):
+                out[f"train_cache_aug_native_t{rt}_pairs_s"] = round(train_rate(ds, batch, 0, native=True, epochs=3,
+                                                                                 read_threads=rt), 1)
+            hi = torch.cuda.Stream(priority=-1)
+            with torch.cuda.stream(hi):
+                out["train_cache_aug_native_hiprio_pairs_s"] = round(train_rate(ds, batch, 0, native=True, epochs=3), 1)
+            print(f"experiments: {out}", file=sys.stderr, flush=True)
         for name, (ds, workers, native) in arms.items():
-            r = train_rate(ds, batch, workers, native=native, epochs=3)
+            r = train_rate(ds, batch, workers, native=native, epochs=2)
             out[f"train_{name}_pairs_s"] = round(r, 1)
             out[f"train_{name}_frac_of_resident"] = round(r / out["resident_pairs_s"], 3)
             print(f"{name}: {out}", file=sys.stderr, flush=True)
