@@ -147,6 +147,14 @@ const char* sd_wgrad_bnbwd_kernel_name(const sd_src* a, const sd_src* b, int M, 
  *   SD_W_CONV3: M = co, N = 9*ci_pad -> dw[co][ci_real][3][3]
  *   SD_W_CONVT: M = ci, N = 4*co     -> dw[ci][co][2][2] */
 int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw, sd_stream s);
+/* up to 48 of those reduces in ONE launch, each bit-identical to its sd_wgrad_reduce call (the slabs must be
+ * distinct buffers: the engine defers a step's reduces into one launch per gradient-ready group) */
+typedef struct sd_wred_job {
+    const float* slab;
+    int splits, M, N, layout, ci_real;
+    float* dw;
+} sd_wred_job;
+int sd_wgrad_reduce_batch(const sd_wred_job* jobs, int njobs, sd_stream s);
 
 /* ---- host data path: the reference's sample cache (dataset.py:86-105 load_cached_sample; cache.py:50-112) ----
  * Reads n np.savez cache files (stored zip of left.npy / right.npy uint8 [H][W][3], disparity.npy f16 [H][W]) with

@@ -85,6 +85,23 @@ class SdPackJob(ctypes.Structure):
 
 _PJOB = ctypes.POINTER(SdPackJob)
 
+
+class SdWredJob(ctypes.Structure):
+    """include/stereo_hip.h: sd_wred_job (one slab reduce of sd_wgrad_reduce_batch)."""
+
+    _fields_ = [
+        ("slab", _p),
+        ("splits", _i),
+        ("M", _i),
+        ("N", _i),
+        ("layout", _i),
+        ("ci_real", _i),
+        ("dw", _p),
+    ]
+
+
+_WJOB = ctypes.POINTER(SdWredJob)
+
 # name -> (restype, argtypes); mirrors include/stereo_hip.h
 PROTOTYPES: dict[str, tuple] = {
     "sd_version": (_i, []),
@@ -109,6 +126,7 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_wgrad_gemm_bnbwd": (_i, [_i, _SRC, _SRC, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
     "sd_wgrad_bnbwd_kernel_name": (ctypes.c_char_p, [_SRC, _SRC, _i, _i]),
     "sd_wgrad_reduce": (_i, [_p, _i, _i, _i, _i, _i, _p, _p]),
+    "sd_wgrad_reduce_batch": (_i, [_WJOB, _i, _p]),
     "sd_bn_fwd_finalize": (_i, [_p, _i, _i, _d, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
     "sd_bn_eval_coeffs": (_i, [_p, _p, _p, _p, _i, _f, _p, _p, _p, _p, _p]),
     "sd_chan_reduce_rows": (_i, [_i64, _i]),

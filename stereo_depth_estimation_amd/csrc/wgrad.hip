@@ -194,15 +194,13 @@ __device__ __forceinline__ void wg_store(float* dw, long long e, float v, int N,
 // few output quads and many splits (up to 512): G = 32 keeps 16 loads per output in flight instead of 4 (the
 // 8-group form was one dependent memory round trip per 32 splits, 9-12 us for layers of a few KB)
 template <int G>
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ slab, int splits, int M, int N,
-                                                      int layout, int ci_pad, int ci_real, float* __restrict__ dw) {
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, int splits, long long total4, int N,
+                                                  int layout, int ci_pad, int ci_real, float* __restrict__ dw,
+                                                  int bid, int nblocks, float4* part) {  // part: [G][256 / G]
     constexpr int QB = 256 / G;  // output quads per block
-    const long long total = (long long)M * N;  // a multiple of 4 (N = 9*ci_pad or 4*co, ci_pad % 8 == 0)
-    const long long total4 = total / 4;
-    __shared__ float4 part[G][QB];
     const int el = threadIdx.x % QB, g = threadIdx.x / QB;
     const float4* s4 = reinterpret_cast<const float4*>(slab);
-    for (long long q0 = (long long)blockIdx.x * QB; q0 < total4; q0 += (long long)gridDim.x * QB) {
+    for (long long q0 = (long long)bid * QB; q0 < total4; q0 += (long long)nblocks * QB) {
         const long long q = q0 + el;
         float4 acc[4];
 #pragma unroll
@@ -230,14 +228,14 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
                 }
             }
         }
-        part[g][el] = make_float4((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y),
-                                  (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z), (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w));
+        part[g * QB + el] = make_float4((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y),
+                                        (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z), (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w));
         __syncthreads();
         if (g == 0 && q < total4) {
-            float4 t = part[0][el];
+            float4 t = part[el];
 #pragma unroll
             for (int k = 1; k < G; ++k) {
-                const float4 v = part[k][el];
+                const float4 v = part[k * QB + el];
                 t.x += v.x;
                 t.y += v.y;
                 t.z += v.z;
@@ -251,6 +249,45 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
         }
         __syncthreads();
     }
+}
+
+// G split groups per block (8 or 32), 256 / G float4 outputs per block, 4 independent accumulators per lane: each
+// output quad sums its splits in a fixed order (deterministic for a given split count and G). Small layers have
+// few output quads and many splits (up to 512): G = 32 keeps 16 loads per output in flight instead of 4 (the
+// 8-group form was one dependent memory round trip per 32 splits, 9-12 us for layers of a few KB)
+template <int G>
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ slab, int splits, int M, int N,
+                                                      int layout, int ci_pad, int ci_real, float* __restrict__ dw) {
+    __shared__ float4 part[256];
+    wgrad_reduce_body<G>(slab, splits, (long long)M * N / 4, N, layout, ci_pad, ci_real, dw, blockIdx.x, gridDim.x,
+                         part);
+}
+
+// Many weight gradients' slab reduces in ONE launch (sd_wgrad_reduce_batch): job j owns blocks [b0, b0 + nblk) and
+// runs exactly the single-job reduce of sd_wgrad_reduce (same G, same block count, so the same summation order and
+// bit-identical gradients). A step's 22 reduces were 22 kernel boundaries with small, low-occupancy tails each.
+constexpr int WRED_MAX = 48;
+struct WRedJob {
+    const float* slab;
+    float* dw;
+    long long total4;
+    int splits, N, layout, ci_pad, ci_real, g32, b0, nblk;
+};
+struct WRedBatch {
+    WRedJob j[WRED_MAX];
+    int n;
+};
+
+__global__ __launch_bounds__(256) void k_wgrad_reduce_batch(const WRedBatch b) {
+    __shared__ float4 part[256];
+    int k = 0;
+    for (int i = 1; i < b.n; ++i) k = (int)blockIdx.x >= b.j[i].b0 ? i : k;  // block-uniform (scalar) job lookup
+    const WRedJob& j = b.j[k];
+    const int bid = blockIdx.x - j.b0;
+    if (j.g32)
+        wgrad_reduce_body<32>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
+    else
+        wgrad_reduce_body<8>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
 }
 
 }  // namespace
@@ -360,30 +397,39 @@ extern "C" int sd_wgrad_gemm_bnbwd(int dtype, const sd_src* a, const sd_src* b, 
     return sd_halo_wgrad(*a, *b, batch, H, W, M, N, slab, splits, to_stream(s), &bn);
 }
 
-extern "C" int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw,
-                               sd_stream s) {
-    SD_REQUIRE(slab && dw && splits > 0 && M > 0 && N > 0, "sd_wgrad_reduce: bad args");
-    SD_REQUIRE(layout == SD_W_CONV3 || layout == SD_W_CONVT, "sd_wgrad_reduce: layout %d", layout);
-    int ci_pad = 0;
+// validation and launch shape of one slab reduce (shared by sd_wgrad_reduce and sd_wgrad_reduce_batch)
+static int wred_plan(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw, const char* what,
+                     int& ci_pad, bool& wide, int& blocks) {
+    SD_REQUIRE(slab && dw && splits > 0 && M > 0 && N > 0, "%s: bad args", what);
+    SD_REQUIRE(layout == SD_W_CONV3 || layout == SD_W_CONVT, "%s: layout %d", what, layout);
+    ci_pad = 0;
     if (layout == SD_W_CONV3) {
-        SD_REQUIRE(N % 9 == 0, "sd_wgrad_reduce: conv3 N=%d not 9*ci", N);
+        SD_REQUIRE(N % 9 == 0, "%s: conv3 N=%d not 9*ci", what, N);
         ci_pad = N / 9;
-        SD_REQUIRE(ci_real > 0 && ci_real <= ci_pad, "sd_wgrad_reduce: ci_real %d", ci_real);
+        SD_REQUIRE(ci_real > 0 && ci_real <= ci_pad, "%s: ci_real %d", what, ci_real);
     } else {
-        SD_REQUIRE(N % 4 == 0, "sd_wgrad_reduce: convT N=%d not 4*co", N);
+        SD_REQUIRE(N % 4 == 0, "%s: convT N=%d not 4*co", what, N);
     }
-    SD_REQUIRE(layout != SD_W_CONV3 || ci_pad % 4 == 0, "sd_wgrad_reduce: ci_pad %d not a multiple of 4", ci_pad);
-    SD_REQUIRE(((uintptr_t)slab & 15) == 0, "sd_wgrad_reduce: slab not 16-B aligned");
+    SD_REQUIRE(layout != SD_W_CONV3 || ci_pad % 4 == 0, "%s: ci_pad %d not a multiple of 4", what, ci_pad);
+    SD_REQUIRE(((uintptr_t)slab & 15) == 0, "%s: slab not 16-B aligned", what);
     const long long total4 = (long long)M * N / 4;
     // 32 split groups where 8 would give less than two blocks per CU (SD_WGRED_G=8 forces the old form, A/B runs)
     static const int g_env = [] {
         const char* e = getenv("SD_WGRED_G");
         return e ? atoi(e) : 0;
     }();
-    const bool wide = g_env ? g_env == 32 : (total4 + 31) / 32 < 512 && splits >= 64;
+    wide = g_env ? g_env == 32 : (total4 + 31) / 32 < 512 && splits >= 64;
     const int qb = wide ? 8 : 32;
-    long long nb = (total4 + qb - 1) / qb;
-    const int blocks = (int)(nb > 8192 ? 8192 : nb);
+    const long long nb = (total4 + qb - 1) / qb;
+    blocks = (int)(nb > 8192 ? 8192 : nb);
+    return 0;
+}
+
+extern "C" int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw,
+                               sd_stream s) {
+    int ci_pad = 0, blocks = 0;
+    bool wide = false;
+    if (int e = wred_plan(slab, splits, M, N, layout, ci_real, dw, "sd_wgrad_reduce", ci_pad, wide, blocks)) return e;
     if (wide)
         hipLaunchKernelGGL(k_wgrad_reduce<32>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
                            ci_pad, ci_real, dw);
@@ -391,4 +437,26 @@ extern "C" int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int 
         hipLaunchKernelGGL(k_wgrad_reduce<8>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
                            ci_pad, ci_real, dw);
     return sd_check_launch("sd_wgrad_reduce");
+}
+
+extern "C" int sd_wgrad_reduce_batch(const sd_wred_job* jobs, int njobs, sd_stream s) {
+    SD_REQUIRE(jobs && njobs >= 0 && njobs <= WRED_MAX, "sd_wgrad_reduce_batch: njobs %d (max %d)", njobs, WRED_MAX);
+    if (njobs == 0) return 0;
+    WRedBatch b{};
+    b.n = njobs;
+    long long total_blocks = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const sd_wred_job& q = jobs[i];
+        int ci_pad = 0, blocks = 0;
+        bool wide = false;
+        if (int e = wred_plan(q.slab, q.splits, q.M, q.N, q.layout, q.ci_real, q.dw, "sd_wgrad_reduce_batch", ci_pad,
+                              wide, blocks))
+            return e;
+        b.j[i] = WRedJob{q.slab, q.dw, (long long)q.M * q.N / 4, q.splits, q.N, q.layout, ci_pad, q.ci_real,
+                         wide ? 1 : 0, (int)total_blocks, blocks};
+        total_blocks += blocks;
+    }
+    SD_REQUIRE(total_blocks < (1LL << 30), "sd_wgrad_reduce_batch: too many blocks");
+    hipLaunchKernelGGL(k_wgrad_reduce_batch, dim3((unsigned)total_blocks), dim3(256), 0, to_stream(s), b);
+    return sd_check_launch("sd_wgrad_reduce_batch");
 }

@@ -79,6 +79,7 @@ class Workspace:
     t: dict = field(default_factory=dict)
     fwd_train: bool = True  # BN mode of the last forward (batch stats vs running stats)
     coeff_key: object = None  # state key the eval-mode BN coefficients in t were computed for
+    slab_off: dict = field(default_factory=dict)  # deferred reduces: each weight gradient's slab region (floats)
 
 
 class UNetEngine:
@@ -167,6 +168,11 @@ class UNetEngine:
         # weight-gradient GEMMs that nothing downstream reads (no fused dy) on that stream too. Two slabs
         # alternate; an event per slab orders its reuse. 0: everything on the current stream.
         self.side_mode = int(os.environ.get("SD_SIDE_REDUCE", "0"))
+        # training: every weight gradient gets its own slab region and the split-K reduces are deferred and run as ONE
+        # launch per gradient-ready group (sd_wgrad_reduce_batch: once per step single-process, once per top-level
+        # module under DDP) instead of one launch per weight; bit-identical sums (SD_DEFER_REDUCE=0: per weight)
+        self.defer_reduce = os.environ.get("SD_DEFER_REDUCE", "1") != "0" and not self.side_mode
+        self._red_jobs: list = []
         self._side: torch.cuda.Stream | None = None
         self._slab_free: list = [None, None]
         self._slab_i = 0
@@ -320,6 +326,20 @@ class UNetEngine:
                     max_chan = max(max_chan, rows * prev.cout * 2)
             max_chan = max(max_chan, L.call("sd_heads_rows", B * H * W) * self.convs["dec1.1"].cout * 2)
             t["chan"] = torch.empty(max_chan, dtype=f32, device=dev)
+            if self.defer_reduce:  # one region per weight gradient (deferred reduces): ~0.7 GB at B=64, 320x240
+                ws.slab_off = {}
+                tot = 0
+                for cl in self.convs.values():
+                    lv = cl.level
+                    sp = L.call("sd_wgrad_splits", dt, B, H >> lv, W >> lv, cl.cout, 9 * cl.cin_pad)
+                    ws.slab_off[cl.name] = tot
+                    tot += _r16(sp * cl.cout * 9 * cl.cin_pad)
+                for u in self.ups.values():
+                    lv = u.level
+                    sp = L.call("sd_wgrad_splits", dt, B, H >> lv, W >> lv, u.cin, 4 * u.cout)
+                    ws.slab_off[u.name] = tot
+                    tot += _r16(sp * u.cin * 4 * u.cout)
+                max_slab = tot
             t["slab"] = torch.empty(max_slab, dtype=f32, device=dev)
             if self.side_mode:
                 t["slab1"] = torch.empty(max_slab, dtype=f32, device=dev)
@@ -598,12 +618,13 @@ class UNetEngine:
         self.bn_sync(glob)
         return loc, glob
 
-    def _wgrad(self, a: L.SdSrc, b: L.SdSrc, lvl: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor):
+    def _wgrad(self, a: L.SdSrc, b: L.SdSrc, lvl: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor,
+               key: str):
         ws, dt = self.ws, self.sd_dtype
         Hl, Wl = ws.H >> lvl, ws.W >> lvl
         sp = L.call("sd_wgrad_splits", dt, ws.B, Hl, Wl, M, N)
         self._wgrad_slabs(lambda slab, st: L.call("sd_wgrad_gemm", dt, a, b, ws.B, Hl, Wl, M, N, slab, sp, st),
-                          sp, M, N, layout, ci_real, dw, gemm_may_side=True)
+                          sp, M, N, layout, ci_real, dw, gemm_may_side=True, key=key)
 
     def _side_stream(self) -> torch.cuda.Stream:
         if self._side is None:
@@ -611,10 +632,17 @@ class UNetEngine:
         return self._side
 
     def _wgrad_slabs(self, gemm, sp: int, M: int, N: int, layout: int, ci_real: int, dw: torch.Tensor,
-                     gemm_may_side: bool):
+                     gemm_may_side: bool, key: str):
         """gemm(slab_ptr, stream) writes sp split-K slabs of an M x N weight gradient; sd_wgrad_reduce sums them
-        into dw. With side_mode the reduce runs on the side stream (and with side_mode 2 a gemm_may_side GEMM too)."""
+        into dw. defer_reduce: the slabs go to the weight's own region and the reduce joins the next batch
+        (_flush_reduces). With side_mode the reduce runs on the side stream (and with side_mode 2 a gemm_may_side GEMM
+        too)."""
         s = self._s()
+        if self.defer_reduce:
+            slab = self.ws.t["slab"].data_ptr() + 4 * self.ws.slab_off[key]
+            gemm(slab, s)
+            self._red_jobs.append(L.SdWredJob(slab, sp, M, N, layout, ci_real, dw.data_ptr()))
+            return
         if not self.side_mode:
             slab = self.ws.t["slab"].data_ptr()
             gemm(slab, s)
@@ -636,6 +664,13 @@ class UNetEngine:
         ev = torch.cuda.Event()
         ev.record(side)
         self._slab_free[i] = ev
+
+    def _flush_reduces(self):
+        """Every deferred slab reduce in one launch (the gradients they write are final after it, in stream order)."""
+        if self._red_jobs:
+            jobs = (L.SdWredJob * len(self._red_jobs))(*self._red_jobs)
+            L.call("sd_wgrad_reduce_batch", jobs, len(self._red_jobs), self._s())
+            self._red_jobs = []
 
     def _side_join(self):
         """The current stream waits for everything queued on the side stream (gradients final)."""
@@ -669,7 +704,7 @@ class UNetEngine:
             # writes dy, which the dgrad below reads: stays on the current stream
             self._wgrad_slabs(lambda slab, st: L.call("sd_wgrad_gemm_bnbwd", dt, a, b, ws.B, Hl, Wl, M, N, *args,
                                                       slab, sp, st),
-                              sp, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key], gemm_may_side=False)
+                              sp, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key], gemm_may_side=False, key=cl.name)
         if need_dgrad:
             dsrc = L.make_src(dy, cl.cout, Hl, Wl, taps=9)
             if cl.idx == 1:
@@ -701,7 +736,7 @@ class UNetEngine:
                        t["dskip:" + up.name].data_ptr(), up.cout, None, t["stats"].data_ptr() if sums else None, s)
                 self._up_bias_rows = (L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cin), cl.cin) if sums else None
         if not fuse:
-            self._wgrad(a, b, cl.level, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key])
+            self._wgrad(a, b, cl.level, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key], cl.name)
 
     def _up_bwd(self, u: UpL):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
@@ -720,7 +755,7 @@ class UNetEngine:
         src_cl = self.convs[UP_SRC[u.name] + ".1"]
         a = L.make_src(t["y:" + src_cl.name], src_cl.cout, Hl, Wl, taps=1, bn0=self._bn(src_cl))
         b = L.make_src(du, u.cout, Hh, Wh, taps=4)
-        self._wgrad(a, b, u.level, u.cin, 4 * u.cout, L.SD_W_CONVT, u.cin, self.grads[u.name + ".weight"])
+        self._wgrad(a, b, u.level, u.cin, 4 * u.cout, L.SD_W_CONVT, u.cin, self.grads[u.name + ".weight"], u.name)
         if self.bnsum_fuse and L.call("sd_conv_gemm_bnsum_ok", dt, b, u.cin) == 1:
             # da of the source conv and its BatchNorm-backward sums (for _bn_bwd(src_cl)) from one launch:
             # the reduce pass over (da, y) that followed every ConvTranspose dgrad is gone
@@ -768,12 +803,14 @@ class UNetEngine:
                 self._up_bwd(self.ups[UP_OF_DEC[blk]])
                 if grad_hook is not None:
                     self._grads_ready(grad_hook, UP_OF_DEC[blk])
+        self._flush_reduces()
         self._side_join()
 
     def _grads_ready(self, grad_hook, name: str):
         """grad_hook(name) with the current stream at a point where `name`'s gradients are final. With side-stream
         reduces that is the side stream once it has caught up with this one: a collective the hook launches then
         waits for the reduces without the current stream waiting for them."""
+        self._flush_reduces()
         if self._side is None:
             grad_hook(name)
             return

@@ -221,6 +221,26 @@ def test_side_stream_reduces_bit_identical(monkeypatch, side):
         assert torch.equal(p0, runs[side][2][k]), k
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_deferred_slab_reduces_bit_identical(monkeypatch, precision):
+    """The step's split-K slab reduces deferred into one sd_wgrad_reduce_batch launch (default) give exactly the
+    gradients, metrics and updated weights of one sd_wgrad_reduce launch per weight (SD_DEFER_REDUCE=0)."""
+    st = U.make_state(32, seed=3)
+    bs = [U.make_batch(2, 96, 128, seed=6), U.make_batch(2, 96, 128, seed=7)]
+    runs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SD_DEFER_REDUCE", mode)
+        m, metrics, _, grads = _fused_two_steps(st, 32, precision, bs)
+        assert m.engine().defer_reduce == (mode == "1")
+        torch.cuda.synchronize()
+        runs[mode] = (metrics, grads, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()})
+    assert runs["0"][0] == runs["1"][0]
+    for k, g0 in runs["0"][1].items():
+        assert torch.equal(g0, runs["1"][1][k]), k
+    for k, p0 in runs["0"][2].items():
+        assert torch.equal(p0, runs["1"][2][k]), k
+
+
 def test_autograd_path_matches_fused_path():
     """model(x) + external loss + loss.backward() (the reference's train.py:328-342 as written)."""
     st = U.make_state(8, seed=0, signed_gamma=True)

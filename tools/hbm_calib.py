@@ -43,9 +43,14 @@ def main():
     flag = torch.zeros(1, dtype=torch.int32, device="cuda")
     n16 = nbytes // 16
     st = torch.cuda.current_stream().cuda_stream
-    for kind, name, mult in ((0, "hip_copy", 2), (1, "hip_read", 1), (2, "hip_fill", 1)):
+    # 3-7: no bounds checks (2 GiB is a multiple of every grid's pass), plain / nontemporal, 4 or 8 loads in flight
+    for kind, name, mult in ((0, "hip_copy", 2), (1, "hip_read", 1), (2, "hip_fill", 1), (3, "hip_copy_nb", 2),
+                             (4, "hip_copy_nb_nt", 2), (5, "hip_copy_nb_nt_u8", 2), (6, "hip_fill_nb_nt", 1),
+                             (7, "hip_fill_nb", 1)):
         best = 0.0
         for blocks in (1024, 2048, 4096, 8192, 16384):
+            if kind >= 3 and n16 % (blocks * 256 * 8):
+                continue
             def run():
                 rc = lib.hbm_run(kind, src.data_ptr(), dst.data_ptr(), n16, blocks, flag.data_ptr(), st)
                 assert rc == 0, rc
