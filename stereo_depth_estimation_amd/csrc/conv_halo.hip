@@ -217,14 +217,16 @@ struct HFwdArgs {
     const float *bsc, *bsh, *bmu, *bis;
 };
 
-#ifndef HC_EPL
-#define HC_EPL 1
-#endif
+// Cache policy of the conv epilogue stores: nontemporal (2). The outputs (0.1-0.3 GB per launch) are read by the next
+// layer's kernel, never again by this one, and allocating them in the XCD's 4 MB L2 evicts the weight rows and halo
+// rows the loaders re-read: A/B over the model's 14 layer shapes (tools/conv_micro.py, same box, two rounds) 1894 ->
+// 1831 us (-3.3 %). Moving the item epilogue to the loader waves instead (they idle 20-60 % at the barrier) was
+// measured too: +1.8 %, the epilogue then delays the next chunk's staging by as much as it saved the MFMA waves.
 #ifndef HC_ST_AUX
-#define HC_ST_AUX 0  // cache-policy bits of the conv epilogue stores (2: nontemporal)
+#define HC_ST_AUX 2
 #endif
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
-constexpr int SBN_MAX = 512;                        // input channels of the forward/dgrad kernel (LDS BN affine)
+constexpr int SBN_MAX = 1024;                       // input channels of the forward/dgrad kernel (LDS BN affine)
 constexpr int HMAX = 384;                           // wgrad halo pixels (>= 17 x 22 for a whole 15x20 image)
 // halo pixels per LDS buffer: 384 (RT 2, and RT 3 at CK 32: 17 x 22 for a whole 15x20 image), 512, 640
 __host__ __device__ constexpr int halo_px_cap(int RT, int CK) { return RT == 4 ? 640 : (RT == 3 && CK == 16 ? 512 : 384); }
@@ -275,16 +277,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     static_assert(IT == 1 || (IT == 2 && HP * IT <= 16), "item masks fit 16 bits");
     constexpr int KS = (9 * CK + 15) / 16;               // 16-deep k-steps per chunk (CK 8: 5, the last half padding)
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
-    // EPL (NT 2 x RT 2 M16 instances, items of >= 2 chunks): the item epilogue runs on the LOADER waves. The MFMA waves
-    // only convert their accumulators to bf16 pixel rows in their scratch region (16 ds_write_b64 per lane) and go on
-    // with the next item; the loaders read the rows back in the iteration after the next barrier, take the BN
-    // statistics and issue the global stores. That epilogue (LDS round trips, address math, statistics VALU, stores)
-    // was 18-46 % of the MFMA waves' cycles at 30x40-240x320 (cycle-counter build, tools/conv_micro.py), time in
-    // which no MFMA issued, while the loader waves sat at the barrier for 20-60 % of theirs.
-    constexpr bool EPL = HC_EPL && M16 && NT == 2 && RT == 2;
-    // epilogue transpose scratch: 32 (M16: 16; EPL: a whole item's 64) pixels x BN channels per MFMA wave (its own
-    // region, no block sync)
-    constexpr int SCR_PX = EPL ? 64 : (M16 ? 16 : 32);
+    // epilogue transpose scratch: 32 (M16: 16) pixels x BN channels per MFMA wave (its own region, no block sync)
+    constexpr int SCR_PX = M16 ? 16 : 32;
     __shared__ __attribute__((aligned(16))) __bf16 scr[4 * SCR_PX * BN];
 
     // waves 0-3 land on the 4 different SIMDs (dispatch order 0->2->1->3, measured), and so do 4-7:
@@ -305,9 +299,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = (my_items + IT - 1) / IT * nchunks;  // chunk iterations (block-uniform), IT items each
-    // EPL hand-off needs >= 2 chunks per item: the loaders read an item's rows during the chunk after the next
-    // barrier, and the MFMA waves rewrite the region only after the NEXT item's last chunk
-    const bool epl = EPL && nchunks >= 2;
 #ifndef HC_LS_N32
 #define HC_LS_N32 2
 #endif
@@ -522,77 +513,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         constexpr std::integral_constant<int, 1> S1{};
         constexpr std::integral_constant<int, 2> S2{};
         constexpr std::integral_constant<int, 3> S3{};
-        // ---- EPL: the epilogue of item i, whose last chunk c the MFMA waves finished between barriers B_c and
-        // B_{c+1} (then wrote its rows), in loader iteration c + 2 (between B_{c+1} and B_{c+2}). Loader wave w takes
-        // MFMA wave w's 64 pixels: whole-pixel 16-B pieces, EEPR pixels per store instruction, as the MFMA form.
-        constexpr int EPPP = NT * 4, EEPR = 64 / EPPP, EER = 32 / EEPR;
-        unsigned lrel[EPL ? (RT * EER + 1) / 2 : 1];  // tile-relative (row << 9 | col) per store row, two per register
-        float lown[EPL && STATS ? 16 : 1];             // BN statistics of channels n0 + 8*(lane % EPPP) + q
-        int ep_item = 0, ep_last = nchunks - 1, ldg = 0;
-        if constexpr (EPL) {
-#pragma unroll
-            for (int k = 0; k < (RT * EER + 1) / 2; ++k) lrel[k] = 0xffffffffu;
-#pragma unroll
-            for (int i = 0; i < RT; ++i)
-#pragma unroll
-                for (int r = 0; r < EER; ++r) {
-                    const int m = (wid + 4 * i) * 32 + r * EEPR + lane / EPPP;
-                    const int hm = m / p.tw, wm = m - hm * p.tw;
-                    const unsigned v = m < mvalid ? (unsigned)((hm << 9) | wm) : 0xffffu;
-                    const int k = i * EER + r;
-                    lrel[k / 2] = (lrel[k / 2] & ~(0xffffu << (16 * (k & 1)))) | (v << (16 * (k & 1)));
-                }
-#pragma unroll
-            for (int k = 0; k < (EPL && STATS ? 16 : 1); ++k) lown[k] = 0.f;
-        }
-        auto epilogue = [&](int item) __attribute__((always_inline)) {
-            const int sp = slot + item * p.gper;
-            const int b = sp / p.tiles, tl = sp - b * p.tiles;
-            const int ty = tl / p.tiles_x;
-            const int h0 = ty * p.th, w0 = (tl - ty * p.tiles_x) * p.tw;
-            const bool split = p.epi == SD_EPI_SPLIT || p.epi == SD_EPI_SPLIT_STATS;
-            const int ns = split ? p.n_split : p.N;
-            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(p.out0 + (size_t)b * hw_img * ns), (short)0, hw_img * ns * 2, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(split ? p.out1 + (size_t)b * hw_img * (p.N - ns) : p.out0), (short)0,
-                split ? hw_img * (p.N - ns) * 2 : 0, 0x00020000);
-            const __bf16* scl = scr + wid * SCR_PX * BN;
-            const int j = lane % EPPP;
-            uint4 v[RT * EER];  // every row read first: one LDS round trip per item, not per store
-#pragma unroll
-            for (int k = 0; k < RT * EER; ++k) {
-                const int px = (k / EER) * 32 + (k % EER) * EEPR + lane / EPPP;
-                v[k] = *reinterpret_cast<const uint4*>(scl + px * BN + (j ^ (px & 7)) * 8);
-            }
-#pragma unroll
-            for (int k = 0; k < RT * EER; ++k) {
-                const unsigned rel = (lrel[k / 2] >> (16 * (k & 1))) & 0xffffu;
-                const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
-                const bool live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
-                const bool in = live & !(WG_EXP & 4096);
-                const int pix = h * p.W + w, c = n0 + j * 8;
-                if constexpr (STATS) {
-                    const unsigned wv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float lo = live ? __uint_as_float(wv[q] << 16) : 0.f;
-                        const float hi = live ? __uint_as_float(wv[q] & 0xffff0000u) : 0.f;
-                        lown[4 * q] += lo;
-                        lown[4 * q + 1] = __builtin_fmaf(lo, lo, lown[4 * q + 1]);
-                        lown[4 * q + 2] += hi;
-                        lown[4 * q + 3] = __builtin_fmaf(hi, hi, lown[4 * q + 3]);
-                    }
-                }
-                __attribute__((ext_vector_type(4))) unsigned data = {v[k].x, v[k].y, v[k].z, v[k].w};
-                // both stores every row (no branch between rows): out of range = dropped, no traffic
-                const unsigned o0 = (in & (c < ns)) ? (unsigned)(pix * ns + c) * 2u : 0x80000000u;
-                const unsigned o1 = (in & split & (c >= ns) & (c < p.N)) ? (unsigned)(pix * (p.N - ns) + c - ns) * 2u
-                                                                         : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b128(data, rs0, o0, 0, HC_ST_AUX);
-                if (split) __builtin_amdgcn_raw_buffer_store_b128(data, rs1, o1, 0, HC_ST_AUX);
-            }
-        };
         constexpr bool DG = (WG_EXP & 1024) != 0;
         unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
         auto stamp = [&](unsigned long long& acc_) __attribute__((always_inline)) {
@@ -607,14 +527,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         };
         auto iter = [&](auto U) __attribute__((always_inline)) {
             if (DG) t0 = __builtin_amdgcn_s_memtime();
-            if constexpr (EPL) {
-                if (epl && ldg - 2 == ep_last && ep_item < my_items) {  // block-uniform
-                    epilogue(ep_item);
-                    ++ep_item;
-                    ep_last += nchunks;
-                }
-                ++ldg;
-            }
             if (!(WG_EXP & 65536)) store(U, decltype(U)::value & 1);
             stamp(t_st);
             if constexpr (!WCONST) if (!(WG_EXP & 65536)) load_w();
@@ -665,27 +577,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             d[2] = t_br;
             d[3] = __builtin_amdgcn_s_memtime() - t_all;
         }
-        if constexpr (EPL) {
-            if (epl) {
-                __syncthreads();  // E1: the MFMA waves have written the rows of the block's last item
-                while (ep_item < my_items) {
-                    epilogue(ep_item);
-                    ++ep_item;
-                }
-                if constexpr (STATS) {  // lanes l, l + EPPP, ... hold the same 8 channels
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-#pragma unroll
-                        for (int o = EPPP; o < 64; o <<= 1) lown[k] += __shfl_xor(lown[k], o);
-                    }
-                    if (lane < EPPP) {
-#pragma unroll
-                        for (int k = 0; k < 16; ++k) redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] = lown[k];
-                    }
-                }
-            }
-        }
-        __syncthreads();  // stats reduction barrier
+        __syncthreads();  // stats reduction barrier (MFMA waves)
         return;
     }
 
@@ -903,27 +795,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (EPL && epl && ++cc == nchunks) {
-            // hand the item to the loader waves: bf16 pixel rows of this wave's 64 pixels (lane l holds channels
-            // 4 * (l >> 4) + 0..3 of each 16-channel block for pixel l & 15 of each 16-pixel half)
-#pragma unroll
-            for (int i2 = 0; i2 < 2 * RT; ++i2)
-#pragma unroll
-                for (int t = 0; t < 2 * NT; ++t) {
-                    bf16x4 v;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[i2][t][q];
-                    const int px = i2 * 16 + (lane & 15), c = t * 16 + 4 * (lane >> 4);
-                    *reinterpret_cast<uint2*>(scw + px * BN + swz(c >> 3, px) * 8 + (c & 4)) = *reinterpret_cast<uint2*>(&v);
-                }
-            cc = 0;
-            ++pass;
-            if (DG) {
-                const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-                t_ep += t1 - t0;
-                t0 = t1;
-            }
-        } else if (!(EPL && epl) && ++cc == nchunks) {
+        if (++cc == nchunks) {
 #pragma unroll
           for (int u = 0; u < IT; ++u) {
             // ---------------------------------------------------- epilogue of the pass's item u
@@ -1045,9 +917,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         }
     }
     for (int e = total; e < padded; ++e) __syncthreads();  // the loaders' iterations past the last chunk
-    if constexpr (EPL) {
-        if (epl) __syncthreads();  // E1: the loaders take the last item's epilogue
-    }
     if (DG && p.dbg && lane == 0) {
         unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + wid) * 4;
         d[0] = t_cp;
@@ -1058,17 +927,15 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 
     // ---------------------------------------------------------------- BN statistics row
     if constexpr (STATS || BNS) {
-        if (!(EPL && epl)) {  // (EPL: the loader waves hold the statistics)
-            // lanes l, l + PPP, l + 2*PPP, ... hold the same 8 channels (of different pixels)
+        // lanes l, l + PPP, l + 2*PPP, ... hold the same 8 channels (of different pixels)
 #pragma unroll
-            for (int k = 0; k < NOWN; ++k) {
+        for (int k = 0; k < NOWN; ++k) {
 #pragma unroll
-                for (int o = PPP; o < 64; o <<= 1) own[k] += __shfl_xor(own[k], o);
-            }
-            if (lane < PPP) {
+            for (int o = PPP; o < 64; o <<= 1) own[k] += __shfl_xor(own[k], o);
+        }
+        if (lane < PPP) {
 #pragma unroll
-                for (int k = 0; k < NOWN; ++k) redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] = own[k];
-            }
+            for (int k = 0; k < NOWN; ++k) redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] = own[k];
         }
     }
     __syncthreads();
@@ -1404,6 +1271,10 @@ constexpr int WS_PD = 5;                        // tap-steps of fragment read-ah
 // 120x160 M=64 x32 57 -> 53 us, the other shapes 1-3 % faster)
 #define WS_PRIO 1
 #endif
+// cache policy of the fused BatchNorm-backward dy stores (nontemporal, as the conv epilogue's HC_ST_AUX)
+#ifndef WS_ST_AUX
+#define WS_ST_AUX 2
+#endif
 
 // blocks per CU: two for the 32 x 32-channel configuration (72 KB of LDS, <= 128 registers), whose
 // tiles carry little MFMA work and need more loads in flight; one otherwise
@@ -1605,7 +1476,7 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
                     *reinterpret_cast<uint4*>(dys + (dpix0 + (256 / DPP) * i) * DLD + dpiece * 8) = v;
                     __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
                     const unsigned off = (ok & q.wr) ? (unsigned)(q.dbase + dpo[i]) * 2u : OOB;
-                    if (!(WG_EXP & 1048576)) __builtin_amdgcn_raw_buffer_store_b128(data, rdo, off, 0, 0);
+                    if (!(WG_EXP & 1048576)) __builtin_amdgcn_raw_buffer_store_b128(data, rdo, off, 0, WS_ST_AUX);
                 }
             } else {
 #pragma unroll
