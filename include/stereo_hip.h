@@ -280,6 +280,13 @@ typedef struct sd_qsrc {
     float* qshift; /* out [C] */
 } sd_qsrc;
 int sd_fp8_qparams(const sd_qsrc* src, int nsrc, float* act_scale, sd_stream s);
+/* The same conv with STATIC scales (the engine's forwards after its calibration forward, while the model state is
+ * unchanged): act_scale and the sources' folded affines are the ones sd_fp8_qparams left; no min/max rows are
+ * written. Same operands and result contract as sd_conv3x3_fp8 otherwise (N = 32 or a multiple of 64, <= 512 input
+ * channels; a concatenation's first source a multiple of 16 channels). */
+int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
+                  const float* act_scale, int N, int kpad, void* out, sd_stream s);
+const char* sd_conv3x3_q8_kernel_name(int H, int W, int N, int c0, int c1);
 
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----
  * One flat fp32 parameter/gradient/state buffer (all tensors share lr/betas/eps/wd).

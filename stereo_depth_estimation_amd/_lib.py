@@ -152,6 +152,8 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_heads_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "sd_pack_conv3_w_fp8": (_i, [_p, _i, _i, _i, _i, _p, _p, _p]),
     "sd_conv3x3_fp8": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p, _p]),
+    "sd_conv3x3_q8": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p]),
+    "sd_conv3x3_q8_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
     "sd_conv3x3_fp8_rows": (_i, [_i, _i, _i, _i]),
     "sd_conv3x3_fp8_kernel_name": (ctypes.c_char_p, [_i]),
     "sd_chan_minmax_rows": (_i, [_i64, _i]),

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const T* __restrict__ da, 
             const float xh = (yy[i] - mu[i]) * is[i];
             out[i] = k0[i] * (dz - k1[i] - xh * k2[i]);
         }
-        store8(dy + px * C + c, out);
+        store8_nt(dy + px * C + c, out);
     }
 }
 
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void k_pool_bwd_add(const T* __restrict__ y, c
                 zero8(o);
 #pragma unroll
             for (int i = 0; i < 8; ++i) o[i] += (am[i] == k) ? dp[i] : 0.f;
-            store8(da + off[k], o);
+            store8_nt(da + off[k], o);
             if (BNSUM) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {

@@ -107,6 +107,28 @@ __device__ __forceinline__ void store8(__bf16* p, const float (&v)[8]) {
     for (int i = 0; i < 8; ++i) b[i] = (__bf16)v[i];
     *reinterpret_cast<bf16x8*>(p) = b;
 }
+// Streaming output stores of the elementwise kernels (pool backward, BN-backward apply, heads' da, pooled
+// activations, ConvTranspose outputs). Nontemporal (SD_NT_STORES=1) measured 0.6 % slower on the step (same-box A/B,
+// 3 rounds: 6945 vs 6987 pairs/s), unlike the halo conv's epilogue (conv_halo.hip HC_ST_AUX), whose L2 holds re-read
+// weight and halo rows: these kernels re-read nothing, and their outputs are read by the next kernel soon enough to
+// hit in the 256 MB Infinity Cache. Default: plain stores.
+#ifndef SD_NT_STORES
+#define SD_NT_STORES 0
+#endif
+typedef unsigned u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_nt(void* p, uint4 v) {
+    if (SD_NT_STORES)
+        __builtin_nontemporal_store(u32x4_nt{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_nt*>(p));
+    else
+        *reinterpret_cast<uint4*>(p) = v;
+}
+__device__ __forceinline__ void store8_nt(float* p, const float (&v)[8]) { store8(p, v); }
+__device__ __forceinline__ void store8_nt(__bf16* p, const float (&v)[8]) {
+    bf16x8 b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = (__bf16)v[i];
+    store16_nt(p, *reinterpret_cast<uint4*>(&b));
+}
 __device__ __forceinline__ void zero8(float (&v)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = 0.f;

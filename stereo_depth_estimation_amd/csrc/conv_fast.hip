@@ -583,7 +583,7 @@ __global__ __launch_bounds__(256) void k_bnrelu_pool_bf16(const __bf16* __restri
 #pragma unroll
             for (int i = 0; i < 8; ++i) o[i] = k == 0 ? v[i] : fmaxf(o[i], v[i]);
         }
-        store8(out + (size_t)win * C + c, o);
+        store8_nt(out + (size_t)win * C + c, o);
     }
 }
 

@@ -239,10 +239,10 @@ __global__ __launch_bounds__(256, RING > 3 ? 1 : 2) void k_convt(const CtArgs p)
                         const int w = m - bh * p.W, h = bh - b * p.H;
                         const int n = n0 + n8, sub = fdiv(n, p.fC), o = n - sub * p.C;
                         const size_t pix = ((size_t)b * 2 * p.H + 2 * h + (sub >> 1)) * (2 * p.W) + 2 * w + (sub & 1);
-                        *reinterpret_cast<uint4*>(p.out + pix * p.C + o) = v;
+                        store16_nt(p.out + pix * p.C + o, v);
                     }
                 } else {
-                    if (m < p.M) *reinterpret_cast<uint4*>(p.out + (size_t)m * p.N + n0 + n8) = v;
+                    if (m < p.M) store16_nt(p.out + (size_t)m * p.N + n0 + n8, v);
                     if constexpr (BNS) {
                         // the stored (bf16) da: dz = da where y*scale+shift > 0, xhat = (y-mean)*invstd
                         const bool live = m < p.M;

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void k_heads(const T* __restrict__ y, const
                 gw_d[i] += gd * a[u][i];
                 gw_l[i] += gl * a[u][i];
             }
-            if (da) store8(da + px * C + c0, o);
+            if (da) store8_nt(da + px * C + c0, o);
             if constexpr (BNSUM) {
                 float yv[8];
                 raw_to_f32<T>(q.raw[u], yv);

@@ -80,6 +80,9 @@ class Workspace:
     fwd_train: bool = True  # BN mode of the last forward (batch stats vs running stats)
     coeff_key: object = None  # state key the eval-mode BN coefficients in t were computed for
     slab_off: dict = field(default_factory=dict)  # deferred reduces: each weight gradient's slab region (floats)
+    q8_ready: bool = False  # fp8: the activation scales of a calibration forward are in t
+    graph: object = None  # HIP graph of the eval forward (after the input pack) for graph_key = (state key, path)
+    graph_key: object = None
 
 
 class UNetEngine:
@@ -99,6 +102,10 @@ class UNetEngine:
         self._packed_key = None
         self._eval_coeffs = True
         self.fp8 = precision == "fp8"  # bf16 activations, e4m3 3x3 convs (eval forward only)
+        # fp8: static activation scales from a calibration forward per model state (SD_FP8_STATIC=0: dynamic always)
+        self.fp8_static = os.environ.get("SD_FP8_STATIC", "1") != "0"
+        # eval forwards of an unchanged state replay a captured HIP graph (SD_EVAL_GRAPH=0: eager launches)
+        self.eval_graphs = os.environ.get("SD_EVAL_GRAPH", "1") != "0"
         self.sd_dtype = L.SD_F32 if precision == "fp32" else L.SD_BF16
         self.act_dtype = torch.float32 if precision == "fp32" else torch.bfloat16
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -145,6 +152,9 @@ class UNetEngine:
             self.wq8 = torch.zeros(off8, dtype=torch.uint8, device=self.device)
             self.wscale8 = torch.zeros(soff, dtype=torch.float32, device=self.device)
         self.c1 = c[0]
+        # sd_conv3x3_q8's shapes (N = 32 or a multiple of 64, <= 512 input channels): base_channels 32 and its multiples
+        self._q8_shapes = all((cl.cout == 32 or cl.cout % 64 == 0) and cl.cin_pad <= 512 for cl in self.convs.values()) \
+            and all(u.cout % 16 == 0 for u in self.ups.values())
         # persistent small device state
         dev = self.device
         # this rank's valid pixels (sd_count_valid) and the loss normaliser: the same tensor single-process; DDP gives
@@ -220,6 +230,9 @@ class UNetEngine:
             for cl in self.convs.values():
                 L.call("sd_pack_conv3_w_fp8", self.params[cl.w_key].data_ptr(), cl.cout, cl.cin, cl.cin_pad, cl.kpad8,
                        self.wq8.data_ptr() + cl.off8, self.wscale8.data_ptr() + 4 * cl.soff8, s)
+                if self._q8_bf16(cl):  # the static forward's bf16 layers
+                    L.call("sd_pack_conv3_w", dt, self.params[cl.w_key].data_ptr(), cl.cout, cl.cin, cl.cin_pad, 0,
+                           cl.kpad_f, base + cl.off_f * es, s)
             for u in self.ups.values():
                 L.call("sd_pack_convT_w", dt, self.params[u.name + ".weight"].data_ptr(), u.cin, u.cout, 0, u.kpad_f,
                        base + u.off_f * es, s)
@@ -427,10 +440,9 @@ class UNetEngine:
     def _rows(self, key: str) -> int:
         return self.ws.t[key].shape[0]
 
-    def _conv_fwd_fp8(self, cl: ConvL):
-        """One eval-mode conv3x3 + BN coefficients on the fp8 path (model.py:36-41): the input's dynamic
-        scale from its producers' (min, max) rows, then the e4m3 halo conv."""
-        ws, t, s = self.ws, self.ws.t, self._s()
+    def _fp8_src(self, cl: ConvL):
+        """(qsrc list for sd_fp8_qparams, sd_src with the folded quantisation affines) of conv `cl`'s input."""
+        ws, t = self.ws, self.ws.t
         Hl, Wl = ws.H >> cl.level, ws.W >> cl.level
         qs = [t[f"qs{k}:{cl.name}"] for k in range(len(self._fp8_src_chans(cl)))]
         qh = [t[f"qh{k}:{cl.name}"] for k in range(len(qs))]
@@ -456,6 +468,14 @@ class UNetEngine:
                              bn=self._bn(sk), relu=True)]
             src = L.make_src(t["u:" + up.name], up.cout, Hl, Wl, taps=9, bn0=(qs[0], qh[0]), xform0=L.SD_AFFINE,
                              src1=t["y:" + sk.name], c1=sk.cout, bn1=(qs[1], qh[1]))
+        return q, src
+
+    def _conv_fwd_fp8(self, cl: ConvL):
+        """One eval-mode conv3x3 + BN coefficients on the fp8 path (model.py:36-41): the input's dynamic
+        scale from its producers' (min, max) rows, then the e4m3 halo conv."""
+        ws, t, s = self.ws, self.ws.t, self._s()
+        Hl, Wl = ws.H >> cl.level, ws.W >> cl.level
+        q, src = self._fp8_src(cl)
         arr = (L.SdQSrc * len(q))(*q)
         act_scale = t["as:" + cl.name]
         L.call("sd_fp8_qparams", arr, len(q), act_scale.data_ptr(), s)
@@ -469,7 +489,47 @@ class UNetEngine:
                    t["mean:" + cl.name].data_ptr(), t["invstd:" + cl.name].data_ptr(),
                    t["scale:" + cl.name].data_ptr(), t["shift:" + cl.name].data_ptr(), s)
 
+    def _q8_bf16(self, cl: ConvL) -> bool:
+        """Static fp8 forward: the full-resolution 32-channel convs stay bf16 (k_halo_conv). Their 8/32-channel inputs
+        fill a 64-channel e4m3 chunk (one k-step of v_mfma_scale_f32_32x32x64_f8f6f4) an eighth to a half, so e4m3 was
+        slower there (960x720: enc1.0 35 vs 22 us, dec1.0 57 vs 45 us); they hold 20 % of the forward's FLOPs."""
+        return cl.cout == 32 and cl.level == 0
+
+    def _conv_fwd_q8(self, cl: ConvL):
+        """The same conv with the static scales its calibration forward left (sd_conv3x3_q8): one launch."""
+        ws, t = self.ws, self.ws.t
+        if self._q8_bf16(cl):
+            L.call("sd_conv_gemm", L.SD_BF16, self._src_fwd(cl), ws.B, ws.H >> cl.level, ws.W >> cl.level,
+                   self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STORE, t["y:" + cl.name].data_ptr(), None, 0, None,
+                   None, self._s())
+            return
+        _, src = self._fp8_src(cl)
+        L.call("sd_conv3x3_q8", src, ws.B, ws.H >> cl.level, ws.W >> cl.level, self.wq8.data_ptr() + cl.off8,
+               self.wscale8.data_ptr() + 4 * cl.soff8, t["as:" + cl.name].data_ptr(), cl.cout, cl.kpad8,
+               t["y:" + cl.name].data_ptr(), self._s())
+
+    def _forward_q8(self, ws: Workspace):
+        """Static-scale fp8 forward: model state unchanged since the calibration forward (the live app's loop)."""
+        t, s, B, H, W = ws.t, self._s(), ws.B, ws.H, ws.W
+        for blk in BLOCKS_FWD:
+            if blk in UP_OF_DEC:
+                self._up_fwd(self.ups[UP_OF_DEC[blk]])
+            if blk in PREV_ENC:
+                prev = self.convs[PREV_ENC[blk] + ".1"]
+                lv = prev.level
+                L.call("sd_bnrelu_pool", L.SD_BF16, t["y:" + prev.name].data_ptr(), t["scale:" + prev.name].data_ptr(),
+                       t["shift:" + prev.name].data_ptr(), B, H >> lv, W >> lv, prev.cout,
+                       t["pool:" + prev.name].data_ptr(), s)
+            self._conv_fwd_q8(self.convs[blk + ".0"])
+            self._conv_fwd_q8(self.convs[blk + ".1"])
+        return ws
+
     def _forward_fp8(self, ws: Workspace):
+        # calibration: the first forward of a model state (and every one with SD_FP8_STATIC=0) computes each conv
+        # input's scale from the activations (dynamic); the next forwards of that state reuse the scales
+        if self.fp8_static and self._q8_shapes and ws.q8_ready and not self._eval_coeffs:
+            return self._forward_q8(ws)
+        ws.q8_ready = True
         t, s, B, H, W = ws.t, self._s(), ws.B, ws.H, ws.W
         L.call("sd_chan_minmax", t["xin"].data_ptr(), B * H * W, self.cin_pad0, t["mm:xin"].data_ptr(), s)
         for blk in BLOCKS_FWD:
@@ -508,6 +568,30 @@ class UNetEngine:
         self.phase = "fwd"  # read by measurement hooks (bench.py) to tell forward from backward launches
         x = x.contiguous().float()
         L.call("sd_pack_input", self.sd_dtype, x.data_ptr(), B, C, H, W, self.cin_pad0, ws.t["xin"].data_ptr(), self._s())
+        # eval forwards of an unchanged model state (the live app's loop): the launches after the input pack are
+        # captured into a HIP graph on the second such forward and replayed from the third on (one host call instead
+        # of 27-45 ctypes launches; B=1 960x720 forwards were host-bound at ~20 us of GPU time per kernel)
+        gkey = None
+        if not train and self.eval_graphs and not self._eval_coeffs and ws.coeff_key is not None:
+            gkey = (ws.coeff_key, self._fwd_path(ws))
+            if ws.graph is not None and ws.graph_key == gkey:
+                ws.graph.replay()
+                return ws
+        self._forward_body(ws, train)
+        if gkey is not None and gkey[1] == self._fwd_path(ws):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):  # loader threads may use the device
+                self._forward_body(ws, train)
+            ws.graph, ws.graph_key = g, gkey
+        return ws
+
+    def _fwd_path(self, ws: Workspace) -> str:
+        if not self.fp8:
+            return "bf16" if self.sd_dtype == L.SD_BF16 else "fp32"
+        return "q8" if self.fp8_static and self._q8_shapes and ws.q8_ready and not self._eval_coeffs else "fp8"
+
+    def _forward_body(self, ws: Workspace, train: bool):
+        B, H, W = ws.B, ws.H, ws.W
         if self.fp8:
             return self._forward_fp8(ws)
         for blk in BLOCKS_FWD:

@@ -174,6 +174,9 @@ def test_c5_960x720_eval_forward_fp32_bf16_fp8_vs_oracle():
         m = _hip_model(st, prec).eval()
         with torch.inference_mode():
             d, lv = m(x.to(DEV), return_uncertainty=True)
+            if prec == "fp8":  # the live loop's forwards after the calibration one: static scales (sd_conv3x3_q8)
+                d8, lv8 = m(x.to(DEV), return_uncertainty=True)
+                out["fp8 static"] = (d8.cpu(), lv8.cpu())
         out[prec] = (d.cpu(), lv.cpu())
     assert float((out["fp32"][0] - d_ref).abs().max()) < 1e-3
     assert float((out["fp32"][1] - lv_ref).abs().max()) < 1e-3
@@ -181,6 +184,8 @@ def test_c5_960x720_eval_forward_fp32_bf16_fp8_vs_oracle():
     _assert_within("bf16 logvar", out["bf16"][1], lv_ref, lv_ac, 1.0, 1.0)
     _assert_within("fp8 disp", out["fp8"][0], d_ref, d_ac, 6.0, 4.0)
     _assert_within("fp8 logvar", out["fp8"][1], lv_ref, lv_ac, 6.0, 4.0)
+    _assert_within("fp8 static disp", out["fp8 static"][0], d_ref, d_ac, 6.0, 4.0)
+    _assert_within("fp8 static logvar", out["fp8 static"][1], lv_ref, lv_ac, 6.0, 4.0)
 
 
 # ---------------------------------------------------------------------------------------------- C2: B=64

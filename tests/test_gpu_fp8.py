@@ -112,6 +112,8 @@ def _nhwc(x):
     (1, 30, 40, 96, 0, 64, True),      # 1.5 chunks
     (1, 12, 32, 32, 32, 32, False),    # decoder conv0: signed ConvTranspose output + BN/ReLU skip
     (4, 64, 256, 128, 0, 32, True),    # 2 items x 2 chunks per persistent block
+    (1, 20, 40, 192, 0, 64, True),     # 3 chunks: per-chunk weight staging (sd_conv3x3_q8 non-resident weights)
+    (1, 16, 32, 160, 0, 32, True),     # N = 32 with 3 chunks (sd_conv3x3_q8: RT 2 tiles)
 ])
 def test_conv3x3_fp8_matches_emulation(B, H, W, c0, c1, co, relu0):
     lib = L()
@@ -178,6 +180,15 @@ def test_conv3x3_fp8_matches_emulation(B, H, W, c0, c1, co, relu0):
     m = mm.cpu()
     assert torch.equal(m[..., 0].amin(0), got.amin((0, 2, 3)))
     assert torch.equal(m[..., 1].amax(0), got.amax((0, 2, 3)))
+    # the static-scale kernel (sd_conv3x3_q8) with the scales qparams left: same emulation, same bounds
+    out8 = torch.full_like(out, float("nan"))
+    lib.call("sd_conv3x3_q8", src, B, H, W, wq.data_ptr(), ws.data_ptr(), act.data_ptr(), co, kpad, out8.data_ptr(), s)
+    torch.cuda.synchronize()
+    got8 = out8.float().cpu().reshape(B, H, W, co).permute(0, 3, 1, 2)
+    err8 = (got8 - ref).abs()
+    assert torch.isfinite(got8).all()
+    assert float(err8.max()) <= 1e-2 * float(ref.abs().max()), float(err8.max())
+    assert float(err8.mean()) <= 2e-3 * float(ref.abs().mean())
 
 
 def test_fp8_rejects_training_and_plain_gathers():
@@ -210,11 +221,43 @@ def test_fp8_eval_forward_close_to_reference(base, B, H, W, seed):
     m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in st.items()})
     m = m.to(DEV).eval()
     with torch.inference_mode():
+        # the first forward of a model state calibrates (dynamic scales); the next ones reuse its scales
         d, lv = m(torch.as_tensor(b["input"]).to(DEV), return_uncertainty=True)
+        d2, lv2 = m(torch.as_tensor(b["input"]).to(DEV), return_uncertainty=True)
         d_only = m(torch.as_tensor(b["input"]).to(DEV))
-    assert torch.equal(d, d_only)  # deterministic, and the same path without the logvar head output
-    for got, ref in ((d.cpu(), d_ref), (lv.cpu(), lv_ref)):
+    assert torch.equal(d2, d_only)  # deterministic, and the same path without the logvar head output
+    for got, ref in ((d.cpu(), d_ref), (lv.cpu(), lv_ref), (d2.cpu(), d_ref), (lv2.cpu(), lv_ref)):
         assert torch.isfinite(got).all()
         rel = float((got - ref).abs().mean()) / float(ref.abs().mean())
         print(f"fp8 vs fp32 mean rel err {rel:.4f}")
         assert rel <= FP8_MEAN_REL, rel
+    # static vs calibration forward on the same input: the same scales and codes, other accumulation order
+    assert float((d2 - d).abs().mean()) <= 2e-3 * float(d.abs().mean())
+
+
+def test_fp8_static_scales_on_other_frames():
+    """The live app's loop: scales calibrated on one frame, reused on later frames of the same distribution. Each
+    static forward stays within the fp8 bound of the fp32 reference on its own frame, and close to the dynamic
+    (per-frame scale) forward of that frame."""
+    from stereo_depth_estimation_amd.model import StereoUNet
+
+    st = U.make_state(32, seed=5)
+    m = StereoUNet(base_channels=32, precision="fp8")
+    m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in st.items()})
+    m = m.to(DEV).eval()
+    eng = m.engine()
+    net = U.Net(st, base_channels=32)
+    frames = [torch.as_tensor(U.make_batch(1, 240, 320, seed=s)["input"]) for s in (30, 31, 32)]
+    with torch.inference_mode():
+        m(frames[0].to(DEV))  # calibration
+        for x in frames[1:]:
+            d, lv = m(x.to(DEV), return_uncertainty=True)
+            with torch.no_grad():
+                d_ref, lv_ref = net.forward(x, train=False)
+            for got, ref in ((d.cpu(), d_ref), (lv.cpu(), lv_ref)):
+                rel = float((got - ref).abs().mean()) / float(ref.abs().mean())
+                assert rel <= FP8_MEAN_REL, rel
+            eng.fp8_static = False
+            d_dyn = m(x.to(DEV))
+            eng.fp8_static = True
+            assert float((d - d_dyn).abs().mean()) <= 0.02 * float(d_dyn.abs().mean())

@@ -277,12 +277,12 @@ def test_eval_forward_reuses_packs_and_tracks_weight_changes(precision):
     st2 = {k: torch.as_tensor(np.asarray(v)) for k, v in U.make_state(8, seed=2).items()}
     x = torch.as_tensor(U.make_batch(2, 32, 48, seed=4)["input"]).to(DEV)
 
-    def fresh(state):
+    def fresh(state):  # the first forward of a state and a repeat (fp8: calibration, then its static scales)
         f = StereoUNet(base_channels=8, precision=precision)
         f.load_state_dict(state)
         f = f.to(DEV).eval()
         with torch.inference_mode():
-            return f(x, return_uncertainty=True)
+            return f(x, return_uncertainty=True), f(x, return_uncertainty=True)
 
     m = StereoUNet(base_channels=8, precision=precision)
     m.load_state_dict(st)
@@ -295,14 +295,17 @@ def test_eval_forward_reuses_packs_and_tracks_weight_changes(precision):
     def same(a, b):
         return all(torch.equal(p, q) for p, q in zip(a, b))
 
+    def both(ref):
+        return same(run(), ref[0]) and same(run(), ref[1])
+
     ref1 = fresh(st)
-    assert same(run(), ref1) and same(run(), ref1)  # second call uses the cached packs
+    assert both(ref1)  # second call uses the cached packs (fp8: and the calibrated scales)
     m.load_state_dict(st2)
-    assert same(run(), fresh(st2))
+    assert both(fresh(st2))
     with torch.no_grad():
         m.enc1.block[0].weight.mul_(0.5)
     edited = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    assert same(run(), fresh(edited))
+    assert both(fresh(edited))
     if precision == "fp8":
         return
     # a train-mode step: running statistics (sd_bn_fwd_finalize) and weights (sd_adamw) change on the device
@@ -316,7 +319,7 @@ def test_eval_forward_reuses_packs_and_tracks_weight_changes(precision):
     m.eval()
     after = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     assert not torch.equal(after["enc1.block.0.weight"], edited["enc1.block.0.weight"])
-    assert same(run(), fresh(after))
+    assert both(fresh(after))
 
 
 def test_640x480_forward_fp32_and_bf16_vs_oracle():
