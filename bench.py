@@ -119,7 +119,8 @@ class GemmTimer:
                 self._fwd_conv = 0
         else:
             start, flops, kname = self.cur
-            self.pending.append((kname, flops, start, ev, name, self._shape(name, args)))
+            nbytes = self._min_bytes(args) if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum") else 0.0
+            self.pending.append((kname, flops, start, ev, name, self._shape(name, args), nbytes))
             if name == "sd_conv_gemm" and self._last_phase == "fwd":
                 # forward order (model.py:79-104): the first 10 3x3 convs are enc1..enc4, bottleneck
                 if self._fwd_conv < 10 and args[1].taps == 9:
@@ -174,7 +175,7 @@ class GemmTimer:
     def per_layer(self, steps):
         self.torch.cuda.synchronize()
         agg = defaultdict(lambda: [0, 0.0, 0.0, ""])
-        for kname, flops, a, b, name, shape in self.pending:
+        for kname, flops, a, b, name, shape, _ in self.pending:
             r = agg[shape]
             r[0] += 1
             r[1] += flops
@@ -185,18 +186,20 @@ class GemmTimer:
 
     def summary(self, steps):
         self.torch.cuda.synchronize()
-        agg = defaultdict(lambda: [0, 0.0, 0.0])  # launches, flops, ms
-        for kname, flops, a, b, _, _ in self.pending:
+        agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # launches, flops, ms, algorithmic bytes
+        for kname, flops, a, b, _, _, nbytes in self.pending:
             r = agg[kname]
             r[0] += 1
             r[1] += flops
             r[2] += a.elapsed_time(b)
-        rows = sorted(((v[2], k, v[0], v[1]) for k, v in agg.items()), reverse=True)
+            r[3] += nbytes
+        rows = sorted(((v[2], k, v[0], v[1], v[3]) for k, v in agg.items()), reverse=True)
         if os.environ.get("SD_BENCH_LAYERS"):
             for r in self.per_layer(steps):
                 log(json.dumps(r))
         return [{"kernel": k, "launches_per_step": n / steps, "avg_us": 1e3 * ms / n, "flops_per_launch": fl / n,
-                 "tflops": fl / (ms * 1e-3) / 1e12, "ms_per_step": ms / steps} for ms, k, n, fl in rows]
+                 "alg_bytes_per_launch": by / n if by else None, "tflops": fl / (ms * 1e-3) / 1e12,
+                 "ms_per_step": ms / steps} for ms, k, n, fl, by in rows]
 
 
 def lib_sha256() -> str:
@@ -297,7 +300,12 @@ def infer_fp8(torch, model, dev, H=720, W=960, iters=20):
            "ms_fp8": round(ms["fp8"], 4), "ms_bf16": round(ms["bf16"], 4), "ms_fp32": round(ms["fp32"], 4),
            "pairs_per_s_fp8": round(1e3 / ms["fp8"], 2), "fwd_gflop": 255.87,
            "tflops_fp8": round(255.87e9 / (ms["fp8"] * 1e-3) / 1e12, 1),
-           "mean_disparity_fp32": round(float(d32.mean()), 4)}
+           "mean_disparity_fp32": round(float(d32.mean()), 4),
+           "fp8_path": "e4m3 3x3 convs at 480x360 and below (80 % of the forward's FLOPs) with static activation scales "
+                       "from the first (calibration) forward of the model state; full-res 32-channel convs, ConvTranspose "
+                       "and heads bf16",
+           "timing": f"mean of {iters} forwards after 3 (calibration, capture, replay): each precision's eval forward "
+                     "replays a captured HIP graph"}
     for prec in ("fp8", "bf16"):
         res[f"epe_{prec}_vs_fp32"] = round(float((out[prec][0] - d32).abs().mean()), 5)
     return res
@@ -460,10 +468,16 @@ def main():
         kern = timer.summary(args.steps)
         top = kern[0]
         traffic, tsrc = pmc_traffic(top["kernel"])
-        # arithmetic intensity against the ridge (peak FLOP/s / 8 TB/s); the layer map puts this family above it
+        # arithmetic intensity against the ridge (peak FLOP/s / 8 TB/s): from the PMC bytes of this build when present,
+        # else from the algorithmic bytes (inputs and output once, bf16, + weights: SURVEY §8d)
         ai = top["flops_per_launch"] / traffic if traffic else None
+        alg = top.get("alg_bytes_per_launch")
+        ai_alg = top["flops_per_launch"] / alg if alg else None
+        ai_b = ai if ai is not None else ai_alg
         result["roofline"] = {
-            "bound": "mfma" if ai is None or ai >= peak * 1e12 / 8e12 else "hbm",
+            "bound": ("mfma" if ai_b >= peak * 1e12 / 8e12 else "hbm") if ai_b is not None else None,
+            "alg_bytes_per_launch": alg,
+            "flop_per_alg_byte": round(ai_alg, 1) if ai_alg else None,
             "kernel": top["kernel"],
             "achieved": round(top["tflops"], 2),
             "peak": peak,
