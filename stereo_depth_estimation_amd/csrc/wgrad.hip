@@ -228,8 +228,19 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
                 }
             }
         }
-        part[g * QB + el] = make_float4((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y),
+        const float4 sum4 = make_float4((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y),
                                         (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z), (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w));
+        if constexpr (G == 1) {  // one thread per output quad: no cross-thread sum
+            if (q < total4) {
+                const long long e = 4 * q;
+                wg_store(dw, e, sum4.x, N, layout, ci_pad, ci_real);
+                wg_store(dw, e + 1, sum4.y, N, layout, ci_pad, ci_real);
+                wg_store(dw, e + 2, sum4.z, N, layout, ci_pad, ci_real);
+                wg_store(dw, e + 3, sum4.w, N, layout, ci_pad, ci_real);
+            }
+            continue;
+        }
+        part[g * QB + el] = sum4;
         __syncthreads();
         if (g == 0 && q < total4) {
             float4 t = part[el];
@@ -271,7 +282,7 @@ struct WRedJob {
     const float* slab;
     float* dw;
     long long total4;
-    int splits, N, layout, ci_pad, ci_real, g32, b0, nblk;
+    int splits, N, layout, ci_pad, ci_real, g, b0, nblk;  // g: split groups per block (1, 4, 8 or 32)
 };
 struct WRedBatch {
     WRedJob j[WRED_MAX];
@@ -284,10 +295,14 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_batch(const WRedBatch b) {
     for (int i = 1; i < b.n; ++i) k = (int)blockIdx.x >= b.j[i].b0 ? i : k;  // block-uniform (scalar) job lookup
     const WRedJob& j = b.j[k];
     const int bid = blockIdx.x - j.b0;
-    if (j.g32)
+    if (j.g == 32)
         wgrad_reduce_body<32>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
-    else
+    else if (j.g == 8)
         wgrad_reduce_body<8>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
+    else if (j.g == 4)
+        wgrad_reduce_body<4>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
+    else
+        wgrad_reduce_body<1>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
 }
 
 }  // namespace
@@ -399,7 +414,7 @@ extern "C" int sd_wgrad_gemm_bnbwd(int dtype, const sd_src* a, const sd_src* b, 
 
 // validation and launch shape of one slab reduce (shared by sd_wgrad_reduce and sd_wgrad_reduce_batch)
 static int wred_plan(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw, const char* what,
-                     int& ci_pad, bool& wide, int& blocks) {
+                     int& ci_pad, int& g, int& blocks) {
     SD_REQUIRE(slab && dw && splits > 0 && M > 0 && N > 0, "%s: bad args", what);
     SD_REQUIRE(layout == SD_W_CONV3 || layout == SD_W_CONVT, "%s: layout %d", what, layout);
     ci_pad = 0;
@@ -413,13 +428,16 @@ static int wred_plan(const float* slab, int splits, int M, int N, int layout, in
     SD_REQUIRE(layout != SD_W_CONV3 || ci_pad % 4 == 0, "%s: ci_pad %d not a multiple of 4", what, ci_pad);
     SD_REQUIRE(((uintptr_t)slab & 15) == 0, "%s: slab not 16-B aligned", what);
     const long long total4 = (long long)M * N / 4;
-    // 32 split groups where 8 would give less than two blocks per CU (SD_WGRED_G=8 forces the old form, A/B runs)
-    static const int g_env = [] {
+    static const int g_env = [] {  // SD_WGRED_G=1/4/8/32 forces one form (A/B runs)
         const char* e = getenv("SD_WGRED_G");
-        return e ? atoi(e) : 0;
+        const int v = e ? atoi(e) : 0;
+        return v == 1 || v == 4 || v == 8 || v == 32 ? v : 0;
     }();
-    wide = g_env ? g_env == 32 : (total4 + 31) / 32 < 512 && splits >= 64;
-    const int qb = wide ? 8 : 32;
+    // split groups per block: 32 where 8 would leave fewer than two blocks per CU (small layers, many splits); 1 or 4
+    // where the splits are few (deep layers: 4-64 splits over up to 0.6 M output quads), so that no thread idles and
+    // the blocks stream whole 4-KB rows of each slab instead of summing 32 quads through LDS
+    g = g_env ? g_env : ((total4 + 31) / 32 < 512 && splits >= 64 ? 32 : splits <= 16 ? 1 : splits <= 64 ? 4 : 8);
+    const int qb = 256 / g;
     const long long nb = (total4 + qb - 1) / qb;
     blocks = (int)(nb > 8192 ? 8192 : nb);
     return 0;
@@ -427,14 +445,19 @@ static int wred_plan(const float* slab, int splits, int M, int N, int layout, in
 
 extern "C" int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw,
                                sd_stream s) {
-    int ci_pad = 0, blocks = 0;
-    bool wide = false;
-    if (int e = wred_plan(slab, splits, M, N, layout, ci_real, dw, "sd_wgrad_reduce", ci_pad, wide, blocks)) return e;
-    if (wide)
+    int ci_pad = 0, blocks = 0, g = 8;
+    if (int e = wred_plan(slab, splits, M, N, layout, ci_real, dw, "sd_wgrad_reduce", ci_pad, g, blocks)) return e;
+    if (g == 32)
         hipLaunchKernelGGL(k_wgrad_reduce<32>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
                            ci_pad, ci_real, dw);
-    else
+    else if (g == 8)
         hipLaunchKernelGGL(k_wgrad_reduce<8>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
+                           ci_pad, ci_real, dw);
+    else if (g == 4)
+        hipLaunchKernelGGL(k_wgrad_reduce<4>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
+                           ci_pad, ci_real, dw);
+    else
+        hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(blocks), dim3(256), 0, to_stream(s), slab, splits, M, N, layout,
                            ci_pad, ci_real, dw);
     return sd_check_launch("sd_wgrad_reduce");
 }
@@ -447,13 +470,12 @@ extern "C" int sd_wgrad_reduce_batch(const sd_wred_job* jobs, int njobs, sd_stre
     long long total_blocks = 0;
     for (int i = 0; i < njobs; ++i) {
         const sd_wred_job& q = jobs[i];
-        int ci_pad = 0, blocks = 0;
-        bool wide = false;
+        int ci_pad = 0, blocks = 0, g = 8;
         if (int e = wred_plan(q.slab, q.splits, q.M, q.N, q.layout, q.ci_real, q.dw, "sd_wgrad_reduce_batch", ci_pad,
-                              wide, blocks))
+                              g, blocks))
             return e;
-        b.j[i] = WRedJob{q.slab, q.dw, (long long)q.M * q.N / 4, q.splits, q.N, q.layout, ci_pad, q.ci_real,
-                         wide ? 1 : 0, (int)total_blocks, blocks};
+        b.j[i] = WRedJob{q.slab, q.dw, (long long)q.M * q.N / 4, q.splits, q.N, q.layout, ci_pad, q.ci_real, g,
+                         (int)total_blocks, blocks};
         total_blocks += blocks;
     }
     SD_REQUIRE(total_blocks < (1LL << 30), "sd_wgrad_reduce_batch: too many blocks");
