@@ -225,6 +225,7 @@ struct HFwdArgs {
 #ifndef HC_ST_AUX
 #define HC_ST_AUX 2
 #endif
+template <bool B> struct BoolC { static constexpr bool v = B; };  // a compile-time flag passed to a generic lambda
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
 constexpr int SBN_MAX = 1024;                       // input channels of the forward/dgrad kernel (LDS BN affine)
 constexpr int HMAX = 384;                           // wgrad halo pixels (>= 17 x 22 for a whole 15x20 image)
@@ -815,22 +816,100 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 split ? hw_img * (p.N - ns) * 2 : 0, 0x00020000);
             constexpr int NPART = M16 ? 2 * RT : RT;  // epilogue passes: 16-pixel halves (M16) or 32-pixel tiles
             constexpr int RPP = M16 ? ER / 2 : ER;     // store instructions per pass
+            // one store row: BN statistics of piece v and its 16-B store(s) (32-pixel tile i, store row r)
+            auto row_out = [&](const uint4 v, const int i, const int r, auto SPL) {
+                const int j = lane % PPP;
+                const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
+                const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
+                const bool live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
+                const bool in = live & !(WG_EXP & 4096);
+                const int pix = h * p.W + w, c = n0 + j * 8;
+                if constexpr (BNS) {
+                    const uint4 yv = yq[i * ER + r];
+                    const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
-            for (int i2 = 0; i2 < NPART; ++i2) {
-              const int i = M16 ? i2 >> 1 : i2;        // 32-pixel tile
-              const int r0 = M16 ? (i2 & 1) * RPP : 0;  // its first store row of this pass
-              if constexpr (M16) {
-                // lane l holds channels 4 * (l >> 4) + 0..3 of each 16-channel block for pixel l & 15 of the half:
-                // 8-B pieces into the pixel rows of the scratch (the read-back below takes whole 16-B pieces)
+                    for (int q = 0; q < 4; ++q) {
 #pragma unroll
-                for (int t = 0; t < 2 * NT; ++t) {
-                    bf16x4 v;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[i2][t][q];
-                    const int px = lane & 15, c = t * 16 + 4 * (lane >> 4);
-                    *reinterpret_cast<uint2*>(scw + px * BN + swz(c >> 3, px) * 8 + (c & 4)) = *reinterpret_cast<uint2*>(&v);
+                        for (int hh = 0; hh < 2; ++hh) {
+                            const int ch = 2 * q + hh;
+                            const float d = __uint_as_float(hh ? wv[q] & 0xffff0000u : wv[q] << 16);
+                            const float yy = __uint_as_float(hh ? yw[q] & 0xffff0000u : yw[q] << 16);
+                            const float z = __builtin_fmaf(yy, bk_sc[ch], bk_sh[ch]);
+                            const float dz = (live & (z > 0.f)) ? d : 0.f;
+                            own[4 * q + 2 * hh] += dz;
+                            own[4 * q + 2 * hh + 1] = __builtin_fmaf(dz, (yy - bk_mu[ch]) * bk_is[ch], own[4 * q + 2 * hh + 1]);
+                        }
+                    }
                 }
-              } else {
+                if constexpr (STATS) {
+                    const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float lo = live ? __uint_as_float(wv[q] << 16) : 0.f;
+                        const float hi = live ? __uint_as_float(wv[q] & 0xffff0000u) : 0.f;
+                        own[4 * q] += lo;
+                        own[4 * q + 1] = __builtin_fmaf(lo, lo, own[4 * q + 1]);
+                        own[4 * q + 2] += hi;
+                        own[4 * q + 3] = __builtin_fmaf(hi, hi, own[4 * q + 3]);
+                    }
+                }
+                __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
+                if (!SPL.v) {
+                    const unsigned off = (in & (c < p.N)) ? (unsigned)(pix * p.N + c) * 2u : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b128(data, rs0, off, 0, HC_ST_AUX);
+                } else {  // dgrad of a concatenation: channels < n_split to out0, the rest to out1
+                    const unsigned o0 = (in & (c < ns)) ? (unsigned)(pix * ns + c) * 2u : 0x80000000u;
+                    const unsigned o1 = (in & (c >= ns) & (c < p.N)) ? (unsigned)(pix * (p.N - ns) + c - ns) * 2u
+                                                                   : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b128(data, rs0, o0, 0, HC_ST_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(data, rs1, o1, 0, HC_ST_AUX);
+                }
+            };
+            if constexpr (M16) {
+                // All halves' scratch writes and read-backs issue back to back, then the item's stores: one LDS
+                // round trip per item instead of one per half (LDS is in order per wave, so a half's writes land
+                // after the previous half's reads of the same scratch rows).
+                // (in groups of EG halves where all of them would not fit beside the accumulators)
+                constexpr int EG = (NT == 2 && RT >= 3) ? 2 : NPART;
+                static_assert(NPART % EG == 0, "whole groups of halves");
+                auto epi16 = [&](auto SPL) {
+#pragma unroll
+                  for (int g0 = 0; g0 < NPART; g0 += EG) {
+                    uint4 vv[EG][RPP];
+#pragma unroll
+                    for (int e = 0; e < EG; ++e) {
+                        const int i2 = g0 + e;
+                        // lane l holds channels 4 * (l >> 4) + 0..3 of each 16-channel block for pixel l & 15 of
+                        // the half: 8-B pieces into the pixel rows of the scratch, read back as whole 16-B pieces
+#pragma unroll
+                        for (int t = 0; t < 2 * NT; ++t) {
+                            bf16x4 v;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[i2][t][q];
+                            const int px = lane & 15, c = t * 16 + 4 * (lane >> 4);
+                            *reinterpret_cast<uint2*>(scw + px * BN + swz(c >> 3, px) * 8 + (c & 4)) = *reinterpret_cast<uint2*>(&v);
+                        }
+                        asm volatile("" ::: "memory");  // the reads below after the writes above
+#pragma unroll
+                        for (int rr = 0; rr < RPP; ++rr) {
+                            const int px = rr * EPR + lane / PPP, j = lane % PPP;
+                            vv[e][rr] = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
+                        }
+                        asm volatile("" ::: "memory");  // the next half's writes after these reads
+                    }
+#pragma unroll
+                    for (int e = 0; e < EG; ++e)
+#pragma unroll
+                        for (int rr = 0; rr < RPP; ++rr)
+                            row_out(vv[e][rr], (g0 + e) >> 1, ((g0 + e) & 1) * RPP + rr, SPL);
+                  }
+                };
+                if (split) epi16(BoolC<true>{});
+                else epi16(BoolC<false>{});
+            } else {  // 32x32 tiles, one LDS round trip per tile (this loop through row_out: 8->32 layer 107 -> 141 us)
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+              {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
                     uint2 pk[4];  // this lane's 4 channels of each 8-channel group g4, packed bf16
@@ -855,7 +934,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
 #pragma unroll
                 for (int rr = 0; rr < RPP; ++rr) {
-                    const int r = r0 + rr;
+                    const int r = rr;
                     const int px = rr * EPR + lane / PPP, j = lane % PPP;  // pixel within the pass's scratch rows
                     const uint4 v = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
                     const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
@@ -905,6 +984,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     }
                 }
                 asm volatile("" ::: "memory");  // the next tile's writes after these reads
+            }
             }
           }
             cc = 0;

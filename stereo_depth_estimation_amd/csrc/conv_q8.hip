@@ -373,6 +373,9 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.out + (size_t)b * hw_img * p.N), (short)0, hw_img * p.N * 2, 0x00020000);
             const int chq = 4 * (lane >> 5);
+            // all tiles' scratch writes and read-backs issue back to back, then the stores: one LDS round trip per
+            // item (LDS is in order per wave, so a tile's writes land after the previous tile's reads)
+            uint4 rows[RT][ER];
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
 #pragma unroll
@@ -399,12 +402,15 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
                     }
                 }
                 asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
-                uint4 rows[ER];
 #pragma unroll
                 for (int r = 0; r < ER; ++r) {
                     const int px = r * EPR + lane / PPP, j = lane % PPP;
-                    rows[r] = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
+                    rows[i][r] = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
                 }
+                asm volatile("" ::: "memory");  // the next tile's writes after these reads
+            }
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
 #pragma unroll
                 for (int r = 0; r < ER; ++r) {
                     const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
@@ -412,10 +418,10 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
                     const int c = n0 + (lane % PPP) * 8;
                     const bool in = (rel != 0xffffu) & (h < p.H) & (w < p.W) & (c < p.N);
                     const unsigned off = in ? (unsigned)((h * p.W + w) * p.N + c) * 2u : 0x80000000u;
-                    __attribute__((ext_vector_type(4))) unsigned data = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
+                    const uint4 v = rows[i][r];
+                    __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
                     __builtin_amdgcn_raw_buffer_store_b128(data, rs, off, 0, 2);  // nontemporal
                 }
-                asm volatile("" ::: "memory");  // the next tile's writes after these reads
             }
             cc = 0;
             ++item;
