@@ -906,10 +906,14 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 };
                 if (split) epi16(BoolC<true>{});
                 else epi16(BoolC<false>{});
-            } else {  // 32x32 tiles, one LDS round trip per tile (this loop through row_out: 8->32 layer 107 -> 141 us)
+            } else {  // 32x32 tiles: the scratch round trips of TG tiles back to back, then their stores
+                constexpr int TG = BNS ? 1 : (NT == 2 && RT == 4) ? 2 : RT;  // BNS and 4 tiles x 4 rows spill
 #pragma unroll
-            for (int i = 0; i < RT; ++i) {
-              {
+            for (int i0 = 0; i0 < RT; i0 += TG) {
+              uint4 rows[TG][RPP];
+#pragma unroll
+              for (int e = 0; e < TG; ++e) {
+                const int i = i0 + e;
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
                     uint2 pk[4];  // this lane's 4 channels of each 8-channel group g4, packed bf16
@@ -930,13 +934,21 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                         *reinterpret_cast<uint4*>(scw + px * BN + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
                     }
                 }
-              }
                 asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
 #pragma unroll
-                for (int rr = 0; rr < RPP; ++rr) {
-                    const int r = rr;
-                    const int px = rr * EPR + lane / PPP, j = lane % PPP;  // pixel within the pass's scratch rows
-                    const uint4 v = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
+                for (int r = 0; r < RPP; ++r) {
+                    const int px = r * EPR + lane / PPP, j = lane % PPP;  // pixel within the tile's scratch rows
+                    rows[e][r] = *reinterpret_cast<const uint4*>(scw + px * BN + swz(j, px) * 8);
+                }
+                asm volatile("" ::: "memory");  // the next tile's writes after these reads
+              }
+#pragma unroll
+              for (int e = 0; e < TG; ++e) {
+                const int i = i0 + e;
+#pragma unroll
+                for (int r = 0; r < RPP; ++r) {
+                    const int j = lane % PPP;
+                    const uint4 v = rows[e][r];
                     const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
                     const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
                     const bool live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
@@ -983,7 +995,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                         __builtin_amdgcn_raw_buffer_store_b128(data, rs1, o1, 0, HC_ST_AUX);
                     }
                 }
-                asm volatile("" ::: "memory");  // the next tile's writes after these reads
+              }
             }
             }
           }
