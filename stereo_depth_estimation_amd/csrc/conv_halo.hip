@@ -225,6 +225,24 @@ struct HFwdArgs {
 #ifndef HC_ST_AUX
 #define HC_ST_AUX 2
 #endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// BN statistics of one stored 16-B piece (8 bf16 channels; a pixel outside the tile adds zeros): channel pair q's
+// (sum, sum) in own[4q + {0,1}] and (sumsq, sumsq) in own[4q + {2,3}], so each pair is one v_pk_add_f32 and one
+// v_pk_fma_f32
+__device__ __forceinline__ void stats_add(float* own, const uint4 v, const bool live) {
+    const unsigned wv[4] = {live ? v.x : 0u, live ? v.y : 0u, live ? v.z : 0u, live ? v.w : 0u};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const f32x2 x = {__uint_as_float(wv[q] << 16), __uint_as_float(wv[q] & 0xffff0000u)};
+        f32x2 sm = {own[4 * q], own[4 * q + 1]}, sq = {own[4 * q + 2], own[4 * q + 3]};
+        sm += x;
+        sq = __builtin_elementwise_fma(x, x, sq);
+        own[4 * q] = sm.x;
+        own[4 * q + 1] = sm.y;
+        own[4 * q + 2] = sq.x;
+        own[4 * q + 3] = sq.y;
+    }
+}
 template <bool B> struct BoolC { static constexpr bool v = B; };  // a compile-time flag passed to a generic lambda
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
 constexpr int SBN_MAX = 1024;                       // input channels of the forward/dgrad kernel (LDS BN affine)
@@ -607,7 +625,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // lanes sharing channels are reduced once at the end.
     static_assert(!(STATS && BNS), "one kind of stats rows");
     constexpr int NOWN = STATS || BNS ? 16 : 1;
-    float own[NOWN];  // [q*2 + {sum, sumsq}] of channel n0 + 8*(lane % PPP) + q; BNS: {sum dz, sum dz*xhat}
+    // channel n0 + 8*(lane % PPP) + j: BNS own[2j + {0,1}] = {sum dz, sum dz*xhat}; STATS (stats_add) channel pair
+    // j = 2q, 2q+1: own[4q + {0,1}] their sums, own[4q + {2,3}] their sums of squares
+    float own[NOWN];
 #pragma unroll
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
     f32x16 acc[M16 ? 1 : IT][M16 ? 1 : RT][M16 ? 1 : NT];
@@ -636,6 +656,17 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const int k = i * ER + r;
             erel[k / 2] = (erel[k / 2] & ~(0xffffu << (16 * (k & 1)))) | (v << (16 * (k & 1)));
         }
+    // M16: the same pixels as offsets from the tile origin in the image (hm * W + wm, -1 past the tile), for the
+    // epilogue of items whose tile lies inside the image (no per-row bounds or (row, col) arithmetic)
+    constexpr bool EFAST = M16 && !(NT == 2 && RT == 3);  // (2 x 3 tiles: the offsets spill beside the accumulators)
+    constexpr int NEO = EFAST ? RT * ER : 1;
+    int eoff[NEO];
+#pragma unroll
+    for (int k = 0; k < NEO; ++k) {
+        const int m = (wid + 4 * (k / ER)) * 32 + (k % ER) * EPR + lane / PPP;
+        const int hm = m / p.tw, wm = m - hm * p.tw;
+        eoff[k] = m < mvalid ? hm * p.W + wm : -1;
+    }
     __bf16* const scw = scr + wid * SCR_PX * BN;
     // BNS: the lane's 8 channels are fixed (piece lane % PPP): their BatchNorm constants in registers, and the y
     // pieces of an item's stores prefetched while its last chunk is in the matrix core
@@ -817,13 +848,23 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             constexpr int NPART = M16 ? 2 * RT : RT;  // epilogue passes: 16-pixel halves (M16) or 32-pixel tiles
             constexpr int RPP = M16 ? ER / 2 : ER;     // store instructions per pass
             // one store row: BN statistics of piece v and its 16-B store(s) (32-pixel tile i, store row r)
-            auto row_out = [&](const uint4 v, const int i, const int r, auto SPL) {
+            const bool inside = h0 + p.th <= p.H && w0 + p.tw <= p.W;  // the whole tile is in the image
+            const int pix0 = h0 * p.W + w0;
+            auto row_out = [&](const uint4 v, const int i, const int r, auto SPL, auto INS) {
                 const int j = lane % PPP;
-                const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
-                const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
-                const bool live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
+                bool live;
+                int pix;
+                if constexpr (decltype(INS)::v) {
+                    live = eoff[i * ER + r] >= 0;
+                    pix = pix0 + eoff[i * ER + r];
+                } else {
+                    const unsigned rel = (erel[(i * ER + r) / 2] >> (16 * ((i * ER + r) & 1))) & 0xffffu;
+                    const int h = h0 + (int)(rel >> 9), w = w0 + (int)(rel & 511u);
+                    live = (rel != 0xffffu) & (h < p.H) & (w < p.W);
+                    pix = h * p.W + w;
+                }
                 const bool in = live & !(WG_EXP & 4096);
-                const int pix = h * p.W + w, c = n0 + j * 8;
+                const int c = n0 + j * 8;
                 if constexpr (BNS) {
                     const uint4 yv = yq[i * ER + r];
                     const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
@@ -842,16 +883,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     }
                 }
                 if constexpr (STATS) {
-                    const unsigned wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float lo = live ? __uint_as_float(wv[q] << 16) : 0.f;
-                        const float hi = live ? __uint_as_float(wv[q] & 0xffff0000u) : 0.f;
-                        own[4 * q] += lo;
-                        own[4 * q + 1] = __builtin_fmaf(lo, lo, own[4 * q + 1]);
-                        own[4 * q + 2] += hi;
-                        own[4 * q + 3] = __builtin_fmaf(hi, hi, own[4 * q + 3]);
-                    }
+                    stats_add(own, v, live);
                 }
                 __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
                 if (!SPL.v) {
@@ -872,7 +904,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 // (in groups of EG halves where all of them would not fit beside the accumulators)
                 constexpr int EG = (NT == 2 && RT >= 3) ? 2 : NPART;
                 static_assert(NPART % EG == 0, "whole groups of halves");
-                auto epi16 = [&](auto SPL) {
+                auto epi16 = [&](auto SPL, auto INS) {
 #pragma unroll
                   for (int g0 = 0; g0 < NPART; g0 += EG) {
                     uint4 vv[EG][RPP];
@@ -901,11 +933,17 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     for (int e = 0; e < EG; ++e)
 #pragma unroll
                         for (int rr = 0; rr < RPP; ++rr)
-                            row_out(vv[e][rr], (g0 + e) >> 1, ((g0 + e) & 1) * RPP + rr, SPL);
+                            row_out(vv[e][rr], (g0 + e) >> 1, ((g0 + e) & 1) * RPP + rr, SPL, INS);
                   }
                 };
-                if (split) epi16(BoolC<true>{});
-                else epi16(BoolC<false>{});
+                if (split) {
+                    epi16(BoolC<true>{}, BoolC<false>{});
+                } else if constexpr (EFAST) {
+                    if (inside) epi16(BoolC<false>{}, BoolC<true>{});
+                    else epi16(BoolC<false>{}, BoolC<false>{});
+                } else {
+                    epi16(BoolC<false>{}, BoolC<false>{});
+                }
             } else {  // 32x32 tiles: the scratch round trips of TG tiles back to back, then their stores
                 constexpr int TG = BNS ? 1 : (NT == 2 && RT == 4) ? 2 : RT;  // BNS and 4 tiles x 4 rows spill
 #pragma unroll
@@ -972,16 +1010,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                         }
                     }
                     if constexpr (STATS) {
-                        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float lo = live ? __uint_as_float(wv[q] << 16) : 0.f;
-                            const float hi = live ? __uint_as_float(wv[q] & 0xffff0000u) : 0.f;
-                            own[4 * q] += lo;
-                            own[4 * q + 1] = __builtin_fmaf(lo, lo, own[4 * q + 1]);
-                            own[4 * q + 2] += hi;
-                            own[4 * q + 3] = __builtin_fmaf(hi, hi, own[4 * q + 3]);
-                        }
+                        stats_add(own, v, live);
                     }
                     __attribute__((ext_vector_type(4))) unsigned data = {v.x, v.y, v.z, v.w};
                     if (!split) {
@@ -1027,7 +1056,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         }
         if (lane < PPP) {
 #pragma unroll
-            for (int k = 0; k < NOWN; ++k) redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] = own[k];
+            for (int k = 0; k < NOWN; ++k)  // k: channel k / 2, {sum, sumsq} k & 1
+                redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] =
+                    own[STATS ? (k & ~3) | ((k & 1) << 1) | ((k >> 1) & 1) : k];
         }
     }
     __syncthreads();
