@@ -243,6 +243,31 @@ __device__ __forceinline__ void stats_add(float* own, const uint4 v, const bool 
         own[4 * q + 3] = sq.y;
     }
 }
+// BNS: the BatchNorm constants of a channel pair, -mean*invstd folded for xhat = y*invstd + nmi
+struct BnsK {
+    f32x2 sc, sh, is, nmi;
+};
+// BatchNorm-backward sums of one stored 16-B piece of da (8 bf16 channels) and the y piece of the same pixel:
+// dz = da where y*scale+shift > 0 (a pixel outside the tile adds zeros), own[4q + {0,1}] += dz and
+// own[4q + {2,3}] += dz*xhat for channel pair q, in packed fp32 pairs
+__device__ __forceinline__ void bns_add(float* own, const uint4 v, const uint4 yv, const bool live, const BnsK* bk) {
+    const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const f32x2 d = {__uint_as_float(wv[q] << 16), __uint_as_float(wv[q] & 0xffff0000u)};
+        const f32x2 yy = {__uint_as_float(yw[q] << 16), __uint_as_float(yw[q] & 0xffff0000u)};
+        const f32x2 z = __builtin_elementwise_fma(yy, bk[q].sc, bk[q].sh);
+        const f32x2 xh = __builtin_elementwise_fma(yy, bk[q].is, bk[q].nmi);
+        const f32x2 dz = {(live & (z.x > 0.f)) ? d.x : 0.f, (live & (z.y > 0.f)) ? d.y : 0.f};
+        f32x2 sm = {own[4 * q], own[4 * q + 1]}, sx = {own[4 * q + 2], own[4 * q + 3]};
+        sm += dz;
+        sx = __builtin_elementwise_fma(dz, xh, sx);
+        own[4 * q] = sm.x;
+        own[4 * q + 1] = sm.y;
+        own[4 * q + 2] = sx.x;
+        own[4 * q + 3] = sx.y;
+    }
+}
 template <bool B> struct BoolC { static constexpr bool v = B; };  // a compile-time flag passed to a generic lambda
 constexpr int PERSIST_BLOCKS = 256;                 // one block per CU on MI355X
 constexpr int SBN_MAX = 1024;                       // input channels of the forward/dgrad kernel (LDS BN affine)
@@ -625,8 +650,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // lanes sharing channels are reduced once at the end.
     static_assert(!(STATS && BNS), "one kind of stats rows");
     constexpr int NOWN = STATS || BNS ? 16 : 1;
-    // channel n0 + 8*(lane % PPP) + j: BNS own[2j + {0,1}] = {sum dz, sum dz*xhat}; STATS (stats_add) channel pair
-    // j = 2q, 2q+1: own[4q + {0,1}] their sums, own[4q + {2,3}] their sums of squares
+    // channels n0 + 8*(lane % PPP) + 2q, 2q + 1: own[4q + {0,1}] their sums (STATS, stats_add) or sums of dz (BNS,
+    // bns_add), own[4q + {2,3}] their sums of squares or of dz*xhat
     float own[NOWN];
 #pragma unroll
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
@@ -671,17 +696,26 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // BNS: the lane's 8 channels are fixed (piece lane % PPP): their BatchNorm constants in registers, and the y
     // pieces of an item's stores prefetched while its last chunk is in the matrix core
     constexpr int NBK = BNS ? 8 : 1, NYQ = BNS ? RT * ER : 1;
-    float bk_sc[NBK], bk_sh[NBK], bk_mu[NBK], bk_is[NBK];
+    BnsK bk[NBK / 2 > 0 ? NBK / 2 : 1];  // channel pairs (2q, 2q+1)
     uint4 yq[NYQ];
     if constexpr (BNS) {
         const int c = n0 + (lane % PPP) * 8;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const bool cin = c + q < p.N;
-            bk_sc[q] = cin ? p.bsc[c + q] : 0.f;
-            bk_sh[q] = cin ? p.bsh[c + q] : 0.f;
-            bk_mu[q] = cin ? p.bmu[c + q] : 0.f;
-            bk_is[q] = cin ? p.bis[c + q] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+            float v[4][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ch = c + 2 * q + h;
+                const bool cin = ch < p.N;
+                v[0][h] = cin ? p.bsc[ch] : 0.f;
+                v[1][h] = cin ? p.bsh[ch] : 0.f;
+                v[2][h] = cin ? p.bis[ch] : 0.f;
+                v[3][h] = cin ? -p.bmu[ch] * p.bis[ch] : 0.f;
+            }
+            bk[q].sc = f32x2{v[0][0], v[0][1]};
+            bk[q].sh = f32x2{v[1][0], v[1][1]};
+            bk[q].is = f32x2{v[2][0], v[2][1]};
+            bk[q].nmi = f32x2{v[3][0], v[3][1]};
         }
     }
     auto prefetch_y = [&](int itm) __attribute__((always_inline)) {  // the y pieces this lane stores for item itm
@@ -866,21 +900,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 const bool in = live & !(WG_EXP & 4096);
                 const int c = n0 + j * 8;
                 if constexpr (BNS) {
-                    const uint4 yv = yq[i * ER + r];
-                    const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                        for (int hh = 0; hh < 2; ++hh) {
-                            const int ch = 2 * q + hh;
-                            const float d = __uint_as_float(hh ? wv[q] & 0xffff0000u : wv[q] << 16);
-                            const float yy = __uint_as_float(hh ? yw[q] & 0xffff0000u : yw[q] << 16);
-                            const float z = __builtin_fmaf(yy, bk_sc[ch], bk_sh[ch]);
-                            const float dz = (live & (z > 0.f)) ? d : 0.f;
-                            own[4 * q + 2 * hh] += dz;
-                            own[4 * q + 2 * hh + 1] = __builtin_fmaf(dz, (yy - bk_mu[ch]) * bk_is[ch], own[4 * q + 2 * hh + 1]);
-                        }
-                    }
+                    bns_add(own, v, yq[i * ER + r], live, bk);
                 }
                 if constexpr (STATS) {
                     stats_add(own, v, live);
@@ -993,21 +1013,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     const bool in = live & !(WG_EXP & 4096);
                     const int pix = h * p.W + w, c = n0 + j * 8;
                     if constexpr (BNS) {
-                        const uint4 yv = yq[i * ER + r];
-                        const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                            for (int hh = 0; hh < 2; ++hh) {
-                                const int ch = 2 * q + hh;
-                                const float d = __uint_as_float(hh ? wv[q] & 0xffff0000u : wv[q] << 16);
-                                const float yy = __uint_as_float(hh ? yw[q] & 0xffff0000u : yw[q] << 16);
-                                const float z = __builtin_fmaf(yy, bk_sc[ch], bk_sh[ch]);
-                                const float dz = (live & (z > 0.f)) ? d : 0.f;
-                                own[4 * q + 2 * hh] += dz;
-                                own[4 * q + 2 * hh + 1] = __builtin_fmaf(dz, (yy - bk_mu[ch]) * bk_is[ch], own[4 * q + 2 * hh + 1]);
-                            }
-                        }
+                        bns_add(own, v, yq[i * ER + r], live, bk);
                     }
                     if constexpr (STATS) {
                         stats_add(own, v, live);
@@ -1058,7 +1064,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #pragma unroll
             for (int k = 0; k < NOWN; ++k)  // k: channel k / 2, {sum, sumsq} k & 1
                 redf[(wid * BN + lane * 8 + k / 2) * 2 + (k & 1)] =
-                    own[STATS ? (k & ~3) | ((k & 1) << 1) | ((k >> 1) & 1) : k];
+                    own[(k & ~3) | ((k & 1) << 1) | ((k >> 1) & 1)];  // stats_add / bns_add layout
         }
     }
     __syncthreads();
