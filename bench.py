@@ -128,12 +128,16 @@ class GemmTimer:
                     self._fwd_conv += 1
 
     def _min_bytes(self, args):
-        """Minimal HBM bytes of one conv fwd: read input, write output once (bf16), + weights."""
+        """Minimal HBM bytes of one conv-GEMM launch: read the input once, write the output once (bf16),
+        read the weights. The input has B*H*W pixels of the GEMM grid for 1x1 and 3x3 (halo) sources and 4x that for
+        the 2x2 sub-pixel source of a ConvTranspose2d dgrad (taps = 4: the 2x-resolution gradient); the weights are
+        taps x cin x N."""
         s, B, H, W, N = args[1], args[2], args[3], args[4], args[6]
         cin = s.chans[0] + s.chans[1]
         if s.ptr[0] == self.eng.ws.t["xin"].data_ptr():
             cin = self.eng.in_channels
-        return 2.0 * (B * H * W * (cin + N) + 9 * cin * N)
+        in_px = B * H * W * (4 if s.taps == 4 else 1)
+        return 2.0 * (in_px * cin + B * H * W * N + s.taps * cin * N)
 
     def encoder_roofline(self, steps, peak_tflops, hbm_gbs=8000.0):
         """Encoder conv forward (enc1..bottleneck) against the per-layer roofline
@@ -336,16 +340,73 @@ def cpu_baseline(seconds: float, height: int, width: int):
             "sample": f"{n} train steps x {bsz} pairs @{width}x{height} fp32 (oracle restatement of train.py:320-343)"}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus: int, env: dict, argv: list[str]) -> list[str] | None:
+    """How this invocation runs (decided before anything touches a GPU).
+
+    None: run in this process (N=1, or a rank already started by torch.distributed.run). Otherwise the command of a
+    CHILD launcher that starts N rank processes of this script (`python bench.py --gpus N` without WORLD_SIZE: the
+    driver's own BENCH command form); the parent only waits for it and exits with its code, it never execs.
+    A --gpus / WORLD_SIZE mismatch is an error, never a silent one-GPU measurement."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} must be >= 1")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: refusing to measure a different "
+                             "number of GPUs than asked for")
+        return None
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+
+
+def _probe_rank(args):
+    """SD_BENCH_PROBE=1 (the launcher test, tests/test_bench_launch_cpu.py): each rank joins a gloo group, sums the
+    ranks and rank 0 prints one JSON line; no GPU is touched."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    t = torch.tensor([rank + 1.0])
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "rank_sum": float(t.item()),
+                          "local_ranks": os.environ.get("LOCAL_WORLD_SIZE")}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    cmd = launch_plan(args.gpus, dict(os.environ), sys.argv[1:])
+    if cmd is not None:
+        import subprocess
+
+        log(f"--gpus {args.gpus}: starting {args.gpus} rank processes: {' '.join(cmd)}")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        raise SystemExit(subprocess.call(cmd, env=env))
+    if os.environ.get("SD_BENCH_PROBE") == "1":
+        return _probe_rank(args)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if world > 1 and os.environ.get("SD_BENCH_SHARE_DEVICE", "0") != "1" and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
     # SD_BENCH_SHARE_DEVICE=1: every rank on cuda:0 over gloo, a rehearsal of the N > 1 path (buckets, count
     # all-reduce, barriers, max-over-ranks timing) on a one-GPU box; its rate is not a scaling number
     share = world > 1 and os.environ.get("SD_BENCH_SHARE_DEVICE", "0") == "1"

@@ -82,7 +82,11 @@ int sd_pack_convT_w(int dtype, const float* w, int ci, int co, int dgrad, int kp
 /* Every pack of a step in ONE launch (the per-tensor forms above, up to 64 jobs): job j writes
  * out + out_off (elements of dtype) exactly as the per-tensor call of its kind would.
  * The weights it reads are the reference's Conv2d/ConvTranspose2d parameters (model.py:36,39,67-73). */
-enum { SD_PACK_CONV3_FWD = 0, SD_PACK_CONV3_DGRAD = 1, SD_PACK_CONVT_FWD = 2, SD_PACK_CONVT_DGRAD = 3 };
+enum { SD_PACK_CONV3_FWD = 0, SD_PACK_CONV3_DGRAD = 1, SD_PACK_CONVT_FWD = 2, SD_PACK_CONVT_DGRAD = 3,
+       /* bf16 hi/lo pairs of the fp32 weights (w = hi + lo to ~2^-17 relative; sd_conv3x3_wsplit and the doubled-K
+        * ConvTranspose forward): conv3 fwd [co][kpad], k = tap*2*ci_pad + {ci: hi | ci_pad + ci: lo};
+        * convT fwd [(t,o)][kpad], k = {i: hi | ci + i: lo} */
+       SD_PACK_CONV3_FWD_SPLIT = 4, SD_PACK_CONVT_FWD_SPLIT = 5 };
 typedef struct sd_pack_job {
     const float* w; /* fp32 PyTorch layout: conv3 [co][ci][3][3], convT [ci][co][2][2] */
     int kind;
@@ -119,6 +123,22 @@ int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, int W, cons
                        void* out, const void* y, const float* scale, const float* shift, const float* mean,
                        const float* invstd, float* partials, sd_stream s);
 int sd_conv_gemm_bnsum_ok(int dtype, const sd_src* a, int N);
+
+/* The bf16 3x3 convolution (model.py:36,39) of the halo kernel with two precision options for the eval forwards:
+ *  flags & SD_CONV_WSPLIT: the fp32 weights as bf16 hi/lo pairs (sd_pack_weights kind SD_PACK_CONV3_FWD_SPLIT): each
+ *      chunk of input channels meets the hi then the lo halves, so the weights carry fp32 precision into the MFMA
+ *      while the activations stay bf16 (twice the MFMA work). The weights' bf16 rounding is a systematic change of
+ *      the function that shifted the EPE of trained checkpoints by 2e-3..1e-2 px (tools/precision_study.py).
+ *  out_scale / out_shift (both or neither; STORE only): the stored value is bf16(acc*out_scale[n] + out_shift[n]),
+ *      the layer's eval-mode BatchNorm applied before the rounding (model.py:37,40), so consumers apply only the ReLU
+ *      (pass scale 1, shift 0) and bf16 keeps its relative precision on the normalised activation.
+ * epi: SD_EPI_STORE or SD_EPI_STATS (stats as sd_conv_gemm). bf16 3x3 halo shapes only (N = 32 or N % 64 == 0,
+ * unpooled source): sd_conv3x3_ex_ok. */
+enum { SD_CONV_WSPLIT = 1 };
+int sd_conv3x3_ex(const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, int flags,
+                  const float* out_scale, const float* out_shift, void* out, float* stats, sd_stream s);
+int sd_conv3x3_ex_ok(const sd_src* a, int N);
+const char* sd_conv3x3_ex_kernel_name(const sd_src* a, int H, int W, int N, int epi, int flags, int out_affine);
 int sd_conv_gemm_bnsum_rows(const sd_src* a, int batch, int H, int W, int N);
 const char* sd_conv_gemm_bnsum_kernel_name(const sd_src* a, int H, int W, int N);
 

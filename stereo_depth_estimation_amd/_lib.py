@@ -67,6 +67,8 @@ _QSRC = ctypes.POINTER(SdQSrc)
 
 
 SD_PACK_CONV3_FWD, SD_PACK_CONV3_DGRAD, SD_PACK_CONVT_FWD, SD_PACK_CONVT_DGRAD = 0, 1, 2, 3
+SD_PACK_CONV3_FWD_SPLIT, SD_PACK_CONVT_FWD_SPLIT = 4, 5
+SD_CONV_WSPLIT = 1
 
 
 class SdPackJob(ctypes.Structure):
@@ -119,6 +121,9 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_conv_gemm_bnsum_rows": (_i, [_SRC, _i, _i, _i, _i]),
     "sd_conv_gemm_bnsum_kernel_name": (ctypes.c_char_p, [_SRC, _i, _i, _i]),
     "sd_conv_gemm_kernel_name": (ctypes.c_char_p, [_i, _SRC, _i, _i, _i, _i, _i]),
+    "sd_conv3x3_ex": (_i, [_SRC, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "sd_conv3x3_ex_ok": (_i, [_SRC, _i]),
+    "sd_conv3x3_ex_kernel_name": (ctypes.c_char_p, [_SRC, _i, _i, _i, _i, _i, _i]),
     "sd_wgrad_kernel_name": (ctypes.c_char_p, [_i, _SRC, _SRC, _i, _i]),
     "sd_wgrad_splits": (_i, [_i, _i, _i, _i, _i, _i]),
     "sd_wgrad_gemm": (_i, [_i, _SRC, _SRC, _i, _i, _i, _i, _i, _p, _i, _p]),

@@ -275,9 +275,11 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
 bool sd_halo_fwd_ok(const sd_src& a, int N, int epi);
 bool sd_halo_fwd_shape(int N);
 int sd_halo_fwd_rows(int batch, int H, int W, int N);
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns = false);
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns = false, bool wsplit = false,
+                             bool oaff = false);
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
-                     void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns = nullptr);
+                     void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns = nullptr,
+                     bool wsplit = false, const float* osc = nullptr, const float* osh = nullptr);
 int sd_halo_store_rows(int batch, int H, int W, int N, int ctot);
 bool sd_halo_bnsum_ok(const sd_src& a, int N);
 
@@ -404,4 +406,35 @@ extern "C" int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, 
     SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == H && g.Wl == W, "sd_conv_gemm_bnsum: kpad/grid");
     return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, SD_EPI_STORE, out, nullptr, 0, partials, to_stream(s),
                             &bns);
+}
+
+extern "C" int sd_conv3x3_ex_ok(const sd_src* a, int N) {
+    return a && a->taps == 9 && a->xform[0] != SD_AFFINE && a->xform[1] != SD_AFFINE && sd_halo_fwd_ok(*a, N, SD_EPI_STORE)
+               ? 1
+               : 0;
+}
+
+extern "C" const char* sd_conv3x3_ex_kernel_name(const sd_src* a, int H, int W, int N, int epi, int flags, int oaff) {
+    if (!sd_conv3x3_ex_ok(a, N)) return "";
+    return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1], false, (flags & SD_CONV_WSPLIT) != 0, oaff != 0);
+}
+
+extern "C" int sd_conv3x3_ex(const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi,
+                             int flags, const float* out_scale, const float* out_shift, void* out, float* stats,
+                             sd_stream s) {
+    if (int e = validate_src(a, "sd_conv3x3_ex")) return e;
+    SD_REQUIRE(sd_conv3x3_ex_ok(a, N), "sd_conv3x3_ex: bf16 3x3 halo shapes only (N = 32 or N %% 64 == 0)");
+    SD_REQUIRE(epi == SD_EPI_STORE || epi == SD_EPI_STATS, "sd_conv3x3_ex: epi %d (STORE or STATS)", epi);
+    SD_REQUIRE((flags & ~SD_CONV_WSPLIT) == 0, "sd_conv3x3_ex: flags %d", flags);
+    SD_REQUIRE(!out_scale == !out_shift && (!out_scale || epi == SD_EPI_STORE),
+               "sd_conv3x3_ex: the output affine needs both arrays and the STORE epilogue");
+    SD_REQUIRE(batch > 0 && H > 0 && W > 0 && wpack && out && N % 8 == 0 && (epi != SD_EPI_STATS || stats),
+               "sd_conv3x3_ex: bad args");
+    GatherSrc g = make_gather(*a);
+    SD_REQUIRE(g.Hl == H && g.Wl == W, "sd_conv3x3_ex: source grid %dx%d != GEMM grid %dx%d", g.Hl, g.Wl, H, W);
+    const bool ws = (flags & SD_CONV_WSPLIT) != 0;
+    SD_REQUIRE(kpad % 64 == 0 && kpad >= (ws ? 2 : 1) * g.kchunks * 8, "sd_conv3x3_ex: kpad %d < K (%d)", kpad,
+               (ws ? 2 : 1) * g.kchunks * 8);
+    return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, epi, out, nullptr, 0, stats, to_stream(s), nullptr, ws,
+                            out_scale, out_shift);
 }

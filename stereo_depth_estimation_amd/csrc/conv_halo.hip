@@ -200,8 +200,11 @@ struct HFwdArgs {
     int tiles, nsp;       // tiles per image, batch * tiles
     int nblk, gper;       // N-blocks, blocks per N-block (= stats rows)
     int hw, nhalo;        // halo width (tw+2) and pixel count ((th+2)*(tw+2))
-    const __bf16* wp;     // packed [co][kpad], k = tap*ctot + c
+    const __bf16* wp;     // packed [co][kpad], k = tap*ctot + c (wsplit: k = tap*2*ctot + {hi c | ctot + lo c})
     int N, kpad;
+    int wsplit;           // 1: hi/lo bf16 weight pairs (SD_PACK_CONV3_FWD_SPLIT): each item's chunks run twice
+    const float* osc;     // OAFF: the stored value is bf16(acc * osc[n] + osh[n]) (eval BN applied before rounding)
+    const float* osh;
     int epi;
     __bf16* out0;
     __bf16* out1;
@@ -292,8 +295,14 @@ __device__ __forceinline__ int ld_piece(int item) { return (item >> 3) % PPX; }
 
 // IT items (spatial tiles of the same N-block) per pass: every chunk's weights are staged once for IT halos and
 // the MFMA waves keep IT accumulator sets (IT = 2 with CK = 16 halves the weight staging per MFMA)
-template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS>
+// OAFF (eval forwards, sd_conv3x3_ex): the epilogue applies the layer's eval-mode BatchNorm affine before the bf16
+// rounding, so the stored tensor is z = scale*y + shift and its consumers apply only the ReLU. Rounding z instead of y
+// keeps bf16's relative precision on the normalised activation: where a channel's |mean| / std is large (enc1.0: ~4.6
+// on a trained checkpoint) the rounding of y, magnified by scale, was the largest activation error of the bf16 path
+// (tools/precision_study.py: per-batch EPE noise 1.5e-3 -> 5.4e-4 px, as much as fp32 storage would give).
+template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF = false>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
+    static_assert(!(OAFF && (STATS || BNS)), "the affine epilogue stores eval-mode outputs (no statistics)");
     constexpr int BN = 32 * NT;
     constexpr int PPX = CK / 8;                          // 16-B pieces per pixel (and per tap of a weight row)
     // M16 (every CK = 32 instance but the BNS dgrads): v_mfma_f32_16x16x32_bf16, one k-step per tap. Same LDS bytes and
@@ -339,7 +348,13 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // chunks never straddle the two sources (a source's last chunk may be partial): every chunk has one
     // source, one channel stride and one BN affine
     const int nc0 = (p.a.c0 + CK - 1) / CK;
-    const int nchunks = nc0 + (p.a.c1 + CK - 1) / CK;
+    const int ncp = nc0 + (p.a.c1 + CK - 1) / CK;  // chunks of the input channels
+    // wsplit: an item runs its ncp chunks twice, against the hi then the lo bf16 halves of fp32 weights (w = hi + lo
+    // to ~2^-17 relative), so the sum over both passes is the product with the fp32 weights: the full-resolution
+    // layers' weight rounding is what moved the bf16 path's EPE (tools/precision_study.py). The MFMA waves see
+    // 2 x ncp chunks per item; only the loaders know which pass a chunk belongs to.
+    const int nchunks = p.wsplit ? 2 * ncp : ncp;
+    const int wct = p.wsplit ? 2 * p.a.ctot : p.a.ctot;  // packed weight channels per tap
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = (my_items + IT - 1) / IT * nchunks;  // chunk iterations (block-uniform), IT items each
@@ -352,6 +367,13 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 
     // the BN affine of every input channel (identity for raw sources), read by the loaders per chunk from LDS
     __shared__ __attribute__((aligned(16))) float sbn[2 * SBN_MAX + 2 * CK];  // + the tail of a partial chunk
+    __shared__ __attribute__((aligned(16))) float oaff[OAFF ? 2 * BN : 4];      // OAFF: [scale | shift] of this N-block
+    if constexpr (OAFF) {
+        for (int c = tid; c < 2 * BN; c += 512) {
+            const int ch = n0 + (c < BN ? c : c - BN);
+            oaff[c] = ch < p.N ? (c < BN ? p.osc : p.osh)[ch] : 0.f;
+        }
+    }
     for (int c = tid; c < p.a.ctot; c += 512) {
         const bool first = c < p.a.c0;
         const int cl = first ? c : c - p.a.c0;
@@ -419,7 +441,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         for (int i = 0; i < W_PER_THREAD; ++i) {
             const int item = ltid + i * 256;
             const int co = item / (9 * PPX), r = item - co * (9 * PPX), tap = r / PPX, sp = r - tap * PPX;
-            woff[i] = ((item < WPIECES) & (n0 + co < p.N)) ? (unsigned)((n0 + co) * p.kpad + tap * p.a.ctot + sp * 8) * 2u
+            woff[i] = ((item < WPIECES) & (n0 + co < p.N)) ? (unsigned)((n0 + co) * p.kpad + tap * wct + sp * 8) * 2u
                                                           : OOB;
             asm volatile("" : "+v"(woff[i]));  // kept in registers, not recomputed per chunk
         }
@@ -456,9 +478,11 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         // layers (64 input channels: enc2.1, dec2.1, enc3.0, dec1.0, ...) re-staged 36-72 KB of weights per item
         int w_cc = 0;  // chunk (within the item) of the next weights to load
         auto load_w = [&]() __attribute__((always_inline)) {  // weights of chunk w_cc -> wr, then advance
-            const bool s1 = w_cc >= nc0;
+            const bool lo = w_cc >= ncp;  // wsplit: the second pass reads the lo halves
+            const int wc = lo ? w_cc - ncp : w_cc;
+            const bool s1 = wc >= nc0;
             const int C = s1 ? p.a.c1 : p.a.c0;
-            const int cl = (s1 ? w_cc - nc0 : w_cc) * CK;
+            const int cl = (s1 ? wc - nc0 : wc) * CK;
             if (++w_cc == nchunks) w_cc = 0;
             unsigned v[W_PER_THREAD];
 #pragma unroll
@@ -470,7 +494,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                     if (cl + sp * 8 >= C) v[i] = OOB;
                 }
             }
-            const int cbg = (s1 ? p.a.c0 : 0) + cl;  // first channel of the chunk in the packed k = tap*ctot + c
+            // first channel of the chunk in the packed k = tap*wct + c (+ ctot for the lo halves)
+            const int cbg = (s1 ? p.a.c0 : 0) + cl + (lo ? p.a.ctot : 0);
 #pragma unroll
             for (int i = 0; i < W_PER_THREAD; ++i) {
                 const auto x = __builtin_amdgcn_raw_buffer_load_b128(wrs, v[i], cbg * 2, 0);
@@ -489,9 +514,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         };
         auto load = [&](auto S) __attribute__((always_inline)) {  // halo of chunk (ld_item, ld_cc) -> register set S, then advance
             HSet& q = set_of(S);
-            const bool s1 = ld_cc >= nc0;
+            const int hc = ld_cc >= ncp ? ld_cc - ncp : ld_cc;  // wsplit: the second pass re-reads the same halo
+            const bool s1 = hc >= nc0;
             const int C = s1 ? p.a.c1 : p.a.c0;
-            const int cl = (s1 ? ld_cc - nc0 : ld_cc) * CK;
+            const int cl = (s1 ? hc - nc0 : hc) * CK;
             q.cb = (s1 ? p.a.c0 : 0) + cl;
             q.bn = (s1 ? p.a.x1 : p.a.x0) == SD_BNRELU;
             const bool cok = cl + lpiece * 8 < C;
@@ -936,9 +962,18 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #pragma unroll
                         for (int t = 0; t < 2 * NT; ++t) {
                             bf16x4 v;
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[i2][t][q];
                             const int px = lane & 15, c = t * 16 + 4 * (lane >> 4);
+                            if constexpr (OAFF) {
+                                const float4 sc = *reinterpret_cast<const float4*>(oaff + c);
+                                const float4 sh = *reinterpret_cast<const float4*>(oaff + BN + c);
+                                v[0] = (__bf16)fmaf(acc4[i2][t][0], sc.x, sh.x);
+                                v[1] = (__bf16)fmaf(acc4[i2][t][1], sc.y, sh.y);
+                                v[2] = (__bf16)fmaf(acc4[i2][t][2], sc.z, sh.z);
+                                v[3] = (__bf16)fmaf(acc4[i2][t][3], sc.w, sh.w);
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc4[i2][t][q];
+                            }
                             *reinterpret_cast<uint2*>(scw + px * BN + swz(c >> 3, px) * 8 + (c & 4)) = *reinterpret_cast<uint2*>(&v);
                         }
                         asm volatile("" ::: "memory");  // the reads below after the writes above
@@ -978,8 +1013,18 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #pragma unroll
                     for (int g4 = 0; g4 < 4; ++g4) {
                         bf16x4 v;
+                        if constexpr (OAFF) {  // rows 8*g4 + 4*(lane >> 5) + q of the 32-channel tile t
+                            const int c = t * 32 + 8 * g4 + 4 * (lane >> 5);
+                            const float4 sc = *reinterpret_cast<const float4*>(oaff + c);
+                            const float4 sh = *reinterpret_cast<const float4*>(oaff + BN + c);
+                            v[0] = (__bf16)fmaf(acc[u][i][t][4 * g4 + 0], sc.x, sh.x);
+                            v[1] = (__bf16)fmaf(acc[u][i][t][4 * g4 + 1], sc.y, sh.y);
+                            v[2] = (__bf16)fmaf(acc[u][i][t][4 * g4 + 2], sc.z, sh.z);
+                            v[3] = (__bf16)fmaf(acc[u][i][t][4 * g4 + 3], sc.w, sh.w);
+                        } else {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[u][i][t][4 * g4 + q];
+                            for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[u][i][t][4 * g4 + q];
+                        }
                         pk[g4] = *reinterpret_cast<uint2*>(&v);
                     }
                     // lanes l and l+32 hold the two 4-channel halves of each 8-channel group of one pixel:
@@ -1917,14 +1962,18 @@ static bool wconst_chunks(int nchunks) {
 }
 
 // the instance as rocprofv3 names it: k_halo_conv<NT, RT, CK, STATS, WCONST> (launch_halo's choice)
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns) {
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns, bool wsplit, bool oaff) {
     static thread_local char buf[64];
     const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
-    const bool wc = wconst_chunks(cdiv(c0, t.ck) + cdiv(c1, t.ck));
+    const bool wc = wconst_chunks((cdiv(c0, t.ck) + cdiv(c1, t.ck)) * (wsplit ? 2 : 1));
     const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
-    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck,
-             stats ? "true" : "false", wconst ? "true" : "false", t.it, bns ? "true" : "false");
+    if (oaff)
+        snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, false, %s, %d, false, true>", N == 32 ? 1 : 2, t.rt, t.ck,
+                 wconst ? "true" : "false", t.it);
+    else
+        snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck,
+                 stats ? "true" : "false", wconst ? "true" : "false", t.it, bns ? "true" : "false");
     return buf;
 }
 
@@ -1933,6 +1982,15 @@ const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool 
 template <int NT, int RT, int CK, int IT = 1>
 static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p, bool bns = false) {
     constexpr bool W0 = CK == 8, W1 = CK != 16;  // the instance for wconst false / true
+    if constexpr (IT == 1 && CK != 16) {
+        if (p.osc) {  // eval forwards with the BN affine in the epilogue (sd_conv3x3_ex)
+            if (wconst ? W1 : W0)
+                hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W1, IT, false, true>), grid, dim3(512), 0, st, p);
+            else
+                hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0, IT, false, true>), grid, dim3(512), 0, st, p);
+            return;
+        }
+    }
     // BN-backward sums (dgrad STORE launches, sd_conv_gemm_bnsum); not NT 2 x RT 3 (the second accumulator set
     // and the prefetched y pieces spill there: sd_halo_bnsum_ok)
     if constexpr (CK == 32 && IT == 1 && !(NT == 2 && RT == 3)) {
@@ -1955,7 +2013,8 @@ static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, cons
 }
 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
-                     void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns) {
+                     void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns, bool wsplit,
+                     const float* osc, const float* osh) {
     const bool st_ = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_);
     HFwdArgs p;
@@ -1972,6 +2031,13 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.wp = (const __bf16*)wpack;
     p.N = N;
     p.kpad = kpad;
+    p.wsplit = wsplit ? 1 : 0;
+    p.osc = osc;
+    p.osh = osh;
+    SD_REQUIRE(!osc || (osh && epi == SD_EPI_STORE && !bns && t.it == 1 && t.ck != 16),
+               "sd_conv_gemm(halo): the affine epilogue is a STORE of a CK 8 / 32 shape");
+    SD_REQUIRE(!wsplit || (!bns && kpad >= 18 * (a.chans[0] + a.chans[1])),
+               "sd_conv_gemm(halo): split weights need kpad >= 18 * channels (and no BN-backward sums)");
     p.epi = epi;
     p.out0 = (__bf16*)out0;
     p.out1 = (__bf16*)out1;
@@ -2002,7 +2068,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
                "sd_conv_gemm(halo): image %dx%d or weights %dx%d too large for 32-bit offsets", H, W, N, kpad);
     const dim3 grid(p.gper * p.nblk);
     const int nch = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck);
-    const bool wc = wconst_chunks(nch);
+    const bool wc = wconst_chunks(nch * (wsplit ? 2 : 1));
     SD_REQUIRE(t.ck != 8 || nch == 1, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
     if (t.ck == 8) {
         if (t.rt == 4) launch_halo<1, 4, 8>(st_, wc, grid, st, p);

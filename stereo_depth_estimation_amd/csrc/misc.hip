@@ -106,6 +106,13 @@ struct PackJobs {
     int first[PACK_MAX_JOBS + 1];
     int n;
 };
+// the hi (lo = 0) or lo (lo = 1) bf16 half of v: hi = bf16(v), lo = bf16(v - hi) (v - hi is exact in fp32), so
+// hi + lo carries ~16 significant bits of v (the split packs; bf16 only)
+template <typename T>
+__device__ __forceinline__ T split_half(float v, int lo) {
+    const float hi = (float)from_f32<T>(v);
+    return from_f32<T>(lo ? v - hi : v);
+}
 template <typename T>
 __global__ __launch_bounds__(256) void k_pack_multi(const PackJobs P, T* __restrict__ out) {
     __shared__ float sw[PACK_LDS_FLOATS];
@@ -151,6 +158,29 @@ __global__ __launch_bounds__(256) void k_pack_multi(const PackJobs P, T* __restr
             for (int q = tid; q < 4 * jb.kpad; q += 256) {
                 const int t = q / jb.kpad, k = q - t * jb.kpad;
                 o[(size_t)(t * co + r) * jb.kpad + k] = from_f32<T>(k < ci ? sw[k * 4 + t] : 0.f);
+            }
+            break;
+        }
+        case SD_PACK_CONV3_FWD_SPLIT: {  // out[r][tap*2ci_pad + {i | ci_pad + i}] = {hi | lo}(w[r][i][tap])
+            const float* src = jb.w + (size_t)r * ci * 9;
+            for (int e = tid; e < ci * 9; e += 256) sw[e] = src[e];
+            __syncthreads();
+            const int wct = 2 * jb.ci_pad;
+            for (int k = tid; k < jb.kpad; k += 256) {
+                const int tap = k / wct, rem = k - tap * wct, lo = rem >= jb.ci_pad, i = rem - lo * jb.ci_pad;
+                o[(size_t)r * jb.kpad + k] = split_half<T>(tap < 9 && i < ci ? sw[i * 9 + tap] : 0.f, lo);
+            }
+            break;
+        }
+        case SD_PACK_CONVT_FWD_SPLIT: {  // out[t*co + r][{i | ci + i}] = {hi | lo}(w[i][r][t]), t = 0..3
+            for (int e = tid; e < ci * 4; e += 256) {
+                const int i = e >> 2, t = e & 3;
+                sw[e] = jb.w[((size_t)i * co + r) * 4 + t];
+            }
+            __syncthreads();
+            for (int q = tid; q < 4 * jb.kpad; q += 256) {
+                const int t = q / jb.kpad, k = q - t * jb.kpad, lo = k >= ci, i = k - lo * ci;
+                o[(size_t)(t * co + r) * jb.kpad + k] = split_half<T>(i < ci ? sw[i * 4 + t] : 0.f, lo);
             }
             break;
         }
@@ -290,9 +320,11 @@ extern "C" int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, vo
     long long blocks = 0;
     for (int j = 0; j < njobs; ++j) {
         const sd_pack_job& q = jobs[j];
-        SD_REQUIRE(q.w && q.kind >= SD_PACK_CONV3_FWD && q.kind <= SD_PACK_CONVT_DGRAD && q.co > 0 && q.ci > 0 &&
+        SD_REQUIRE(q.w && q.kind >= SD_PACK_CONV3_FWD && q.kind <= SD_PACK_CONVT_FWD_SPLIT && q.co > 0 && q.ci > 0 &&
                        q.out_off >= 0 && q.kpad % 64 == 0,
                    "sd_pack_weights: job %d bad args", j);
+        SD_REQUIRE(dtype == SD_BF16 || q.kind < SD_PACK_CONV3_FWD_SPLIT, "sd_pack_weights: job %d: split packs are bf16",
+                   j);
         int groups;  // blocks of this job: one per output row (convT fwd: per o, its 4 rows)
         switch (q.kind) {
             case SD_PACK_CONV3_FWD:
@@ -306,6 +338,16 @@ extern "C" int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, vo
                 break;
             case SD_PACK_CONVT_FWD:
                 SD_REQUIRE(q.ci % 8 == 0 && q.co % 8 == 0 && q.kpad >= q.ci && q.ci * 4 <= PACK_LDS_FLOATS,
+                           "sd_pack_weights: job %d", j);
+                groups = q.co;
+                break;
+            case SD_PACK_CONV3_FWD_SPLIT:
+                SD_REQUIRE(q.ci_pad >= q.ci && q.ci_pad % 8 == 0 && q.kpad >= 18 * q.ci_pad && q.ci * 9 <= PACK_LDS_FLOATS,
+                           "sd_pack_weights: job %d", j);
+                groups = q.co;
+                break;
+            case SD_PACK_CONVT_FWD_SPLIT:
+                SD_REQUIRE(q.ci % 8 == 0 && q.co % 8 == 0 && q.kpad >= 2 * q.ci && q.ci * 4 <= PACK_LDS_FLOATS,
                            "sd_pack_weights: job %d", j);
                 groups = q.co;
                 break;

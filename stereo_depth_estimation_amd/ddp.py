@@ -110,9 +110,6 @@ class DataParallel:
         self.cap = int(bucket_cap_mb * 1024 * 1024 / 4)
         self._ar = None
         self.sync_bn = sync_bn
-        eng = model.engine(next(model.parameters()).device)
-        if eng.count is eng.count_local:  # the loss normaliser becomes the global count, this rank's stays for metrics
-            eng.count = torch.zeros_like(eng.count_local)
         if broadcast:
             self.broadcast_state()
         if sync_bn:
@@ -152,11 +149,12 @@ class DataParallel:
                    count_hook=self._allreduce_count, before_step=ar.wait)
 
     def _allreduce_count(self, count: torch.Tensor):
-        """count := the global valid count (this rank's from the engine's count_local, then a SUM all-reduce). Async:
+        """count := the global valid count (sd_count_valid wrote this rank's into both of the engine's counters; the
+        SUM all-reduce turns `count` into the global one, `count_local` keeps this rank's for the metric sums). Async:
         train_step waits on the handle after the forward, so the collective's latency overlaps it."""
         eng = getattr(getattr(self, "model", None), "_engine", None)
-        if eng is not None and count is not eng.count_local:
-            count.copy_(eng.count_local)
+        if eng is not None and count.data_ptr() == eng.count_local.data_ptr():
+            raise RuntimeError("DDP count all-reduce on the engine's per-rank counter (count aliases count_local)")
         return dist.all_reduce(count, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def sum_metrics(self, t: torch.Tensor) -> torch.Tensor:

@@ -56,6 +56,8 @@ class ConvL:
     kpad8: int = 0  # fp8 weights [cout][kpad8], k = tap*r16(cin_pad) + c
     off8: int = 0
     soff8: int = 0
+    kpad_s: int = 0  # hi/lo split weights (wsplit layers): [cout][kpad_s] in UNetEngine.wsplit_pack, -1 offset: none
+    off_s: int = -1
 
 
 @dataclass
@@ -68,6 +70,8 @@ class UpL:
     kpad_d: int = 0
     off_f: int = 0
     off_d: int = 0
+    kpad_s: int = 0  # hi/lo split forward weights (wsplit layers), -1 offset: none
+    off_s: int = -1
 
 
 @dataclass
@@ -100,10 +104,17 @@ class UNetEngine:
         # and BN coefficients while (epoch, storages, versions) is unchanged
         self.state_epoch = 0
         self._packed_key = None
+        self._split_pack_jobs = None
         self._eval_coeffs = True
         self.fp8 = precision == "fp8"  # bf16 activations, e4m3 3x3 convs (eval forward only)
         # fp8: static activation scales from a calibration forward per model state (SD_FP8_STATIC=0: dynamic always)
         self.fp8_static = os.environ.get("SD_FP8_STATIC", "1") != "0"
+        # fp8 recalibration triggers (_fp8_policy): input amax above margin x the calibration frame's, and age
+        self.fp8_range_margin = float(os.environ.get("SD_FP8_RANGE_MARGIN", "1.25"))
+        self.fp8_recalib_every = int(os.environ.get("SD_FP8_RECALIB_EVERY", "0"))
+        self.fp8_calibrations = self.fp8_range_recalibrations = self._fp8_age = 0
+        self._fp8_flag: torch.Tensor | None = None
+        self._fp8_flag_ev = None
         # eval forwards of an unchanged state replay a captured HIP graph (SD_EVAL_GRAPH=0: eager launches)
         self.eval_graphs = os.environ.get("SD_EVAL_GRAPH", "1") != "0"
         self.sd_dtype = L.SD_F32 if precision == "fp32" else L.SD_BF16
@@ -142,6 +153,35 @@ class UNetEngine:
             off += cin * u.kpad_d
             self.ups[k] = u
         self.wpack = torch.zeros(off, dtype=self.act_dtype, device=self.device)
+        # hi/lo split weights for the bf16 (and fp8's bf16 layers') EVAL forwards: the bf16 rounding of the weights is
+        # a systematic change of the function, and on reference-trained checkpoints it shifted the EPE by 2e-3..1e-2 px
+        # (enc1.0 most: its raw-image input has |mean|/std ~ 4.6; on a better-trained model the deeper layers' share
+        # grows); with every weight as a hi + lo pair the shift over 32 held-out pairs is ~2e-4 px, what remains is the
+        # zero-mean noise of the bf16 activations (tools/precision_study.py). The training forward keeps
+        # plain bf16 weights (the EPE is an eval-mode quantity). SD_WSPLIT=all (default) | fullres (the level-0 layers
+        # only) | 0 (off); SD_WSPLIT_TRAIN=1: in the training forward too.
+        # eval forwards of the bf16 path store z = scale*y + shift (the eval BatchNorm applied in the conv epilogue,
+        # sd_conv3x3_ex out_scale/out_shift) instead of y, so bf16's relative precision sits on the normalised value
+        # (tools/precision_study.py: the per-batch EPE noise of the bf16 activations 1.5e-3 -> 5.4e-4 px, what fp32
+        # storage of y would give); consumers then apply only the ReLU. SD_ZSTORE=0: store y.
+        self.zstore = precision == "bf16" and os.environ.get("SD_ZSTORE", "1") != "0"
+        self._zs: set = set()
+        self._one = torch.ones(16 * base_channels, dtype=torch.float32, device=self.device)
+        self._zero = torch.zeros(16 * base_channels, dtype=torch.float32, device=self.device)
+        mode = os.environ.get("SD_WSPLIT", "all")
+        self.wsplit = precision in ("bf16", "fp8") and mode != "0"
+        self.wsplit_train = self.wsplit and os.environ.get("SD_WSPLIT_TRAIN", "0") == "1"
+        offs = 0
+        if self.wsplit:
+            for cl in self.convs.values():
+                if (cl.level == 0 or mode != "fullres") and (cl.cout == 32 or cl.cout % 64 == 0):  # halo shapes
+                    cl.kpad_s, cl.off_s = _r64(18 * cl.cin_pad), offs
+                    offs += cl.cout * cl.kpad_s
+            for u in self.ups.values():
+                if u.name == "up1" or mode != "fullres":
+                    u.kpad_s, u.off_s = _r64(2 * u.cin), offs
+                    offs += 4 * u.cout * u.kpad_s
+        self.wsplit_pack = torch.zeros(max(offs, 1), dtype=torch.bfloat16, device=self.device)
         if self.fp8:
             off8 = soff = 0
             for cl in self.convs.values():
@@ -157,10 +197,12 @@ class UNetEngine:
             and all(u.cout % 16 == 0 for u in self.ups.values())
         # persistent small device state
         dev = self.device
-        # this rank's valid pixels (sd_count_valid) and the loss normaliser: the same tensor single-process; DDP gives
-        # `count` a tensor of its own, filled from count_local and all-reduced to the global count (ddp.DataParallel)
-        self.count_local = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.count = self.count_local
+        # this rank's valid pixels (metric sums) and the loss normaliser, two ints of one buffer that sd_count_valid
+        # fills together (ncount=2); DDP all-reduces `count` alone to the global count (ddp.DataParallel), so the two
+        # never alias and nothing has to copy one into the other
+        self._counts = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.count_local = self._counts[0:1]
+        self.count = self._counts[1:2]
         self.metrics = torch.zeros(5, dtype=torch.float64, device=dev)
         self.adam_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_scratch = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -236,6 +278,10 @@ class UNetEngine:
             for u in self.ups.values():
                 L.call("sd_pack_convT_w", dt, self.params[u.name + ".weight"].data_ptr(), u.cin, u.cout, 0, u.kpad_f,
                        base + u.off_f * es, s)
+            jobs = self._split_jobs()
+            if jobs:
+                arr = (L.SdPackJob * len(jobs))(*[L.SdPackJob(*j) for j in jobs])
+                L.call("sd_pack_weights", L.SD_BF16, arr, len(jobs), self.wsplit_pack.data_ptr(), s)
             return
         # every bf16/fp32 pack of the step in one launch (job table rebuilt when the parameters move)
         key = tuple(t.data_ptr() for t in self.params.values())
@@ -251,8 +297,34 @@ class UNetEngine:
                 jobs.append((w, L.SD_PACK_CONVT_FWD, u.cout, u.cin, u.cin, u.kpad_f, u.off_f))
                 jobs.append((w, L.SD_PACK_CONVT_DGRAD, u.cout, u.cin, u.cin, u.kpad_d, u.off_d))
             self._pack_jobs = (L.SdPackJob * len(jobs))(*[L.SdPackJob(*j) for j in jobs])
+            sj = self._split_jobs()
+            self._split_pack_jobs = (L.SdPackJob * len(sj))(*[L.SdPackJob(*j) for j in sj]) if sj else None
             self._pack_key = key
         L.call("sd_pack_weights", dt, self._pack_jobs, len(self._pack_jobs), base, s)
+        if self._split_pack_jobs is not None:
+            L.call("sd_pack_weights", L.SD_BF16, self._split_pack_jobs, len(self._split_pack_jobs),
+                   self.wsplit_pack.data_ptr(), s)
+
+    def _split_jobs(self) -> list:
+        """sd_pack_weights jobs of the hi/lo split weights (wsplit layers)."""
+        if not self.wsplit:
+            return []
+        jobs = []
+        for cl in self.convs.values():
+            if cl.off_s >= 0:
+                jobs.append((self.params[cl.w_key].data_ptr(), L.SD_PACK_CONV3_FWD_SPLIT, cl.cout, cl.cin, cl.cin_pad,
+                             cl.kpad_s, cl.off_s))
+        for u in self.ups.values():
+            if u.off_s >= 0:
+                jobs.append((self.params[u.name + ".weight"].data_ptr(), L.SD_PACK_CONVT_FWD_SPLIT, u.cout, u.cin, u.cin,
+                             u.kpad_s, u.off_s))
+        return jobs
+
+    def _ws_ptr(self, off: int) -> int:
+        return self.wsplit_pack.data_ptr() + 2 * off
+
+    def _use_wsplit(self, layer, train: bool) -> bool:
+        return layer.off_s >= 0 and (not train or self.wsplit_train)
 
     def _wp(self, off: int) -> int:
         return self.wpack.data_ptr() + off * self.wpack.element_size()
@@ -364,7 +436,11 @@ class UNetEngine:
 
     # ------------------------------------------------------------------ forward
     def _bn(self, cl: ConvL):
+        """The affine its consumers apply (before the ReLU) to conv `cl`'s stored output: the BatchNorm's (scale,
+        shift), or the identity when the eval forward stored z = scale*y + shift already (self._zs)."""
         t = self.ws.t
+        if cl.name in self._zs:
+            return (self._one[:cl.cout], self._zero[:cl.cout])
         return (t["scale:" + cl.name], t["shift:" + cl.name])
 
     def _src_fwd(self, cl: ConvL) -> L.SdSrc:
@@ -396,10 +472,15 @@ class UNetEngine:
         g, b = self.params[cl.bn_key + ".weight"], self.params[cl.bn_key + ".bias"]
         mean, invstd = t["mean:" + cl.name], t["invstd:" + cl.name]
         scale, shift = t["scale:" + cl.name], t["shift:" + cl.name]
+        split = self._use_wsplit(cl, train) and dt == L.SD_BF16
         if train:
             stats = t["stats"]
-            L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STATS,
-                   y.data_ptr(), None, 0, None, stats.data_ptr(), s)
+            if split:
+                L.call("sd_conv3x3_ex", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s), cl.cout, cl.kpad_s,
+                       L.SD_EPI_STATS, L.SD_CONV_WSPLIT, None, None, y.data_ptr(), stats.data_ptr(), s)
+            else:
+                L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STATS,
+                       y.data_ptr(), None, 0, None, stats.data_ptr(), s)
             rows = L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cout)
             rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
             nbt = self.bufs.get(cl.bn_key + ".num_batches_tracked")
@@ -413,17 +494,33 @@ class UNetEngine:
                        b.data_ptr(), rm.data_ptr(), rv.data_ptr(), L.ptr(nbt), BN_MOMENTUM, BN_EPS, mean.data_ptr(),
                        invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
         else:
-            L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STORE,
-                   y.data_ptr(), None, 0, None, None, s)
-            if self._eval_coeffs:
+            if self._eval_coeffs:  # before the conv: an affine epilogue (zstore) stores with them
                 rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
                 L.call("sd_bn_eval_coeffs", rm.data_ptr(), rv.data_ptr(), g.data_ptr(), b.data_ptr(), cl.cout,
                        BN_EPS, mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
+            zs = self.zstore and dt == L.SD_BF16 and L.call("sd_conv3x3_ex_ok", src, cl.cout) == 1
+            if split or zs:
+                L.call("sd_conv3x3_ex", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s) if split else self._wp(cl.off_f),
+                       cl.cout, cl.kpad_s if split else cl.kpad_f, L.SD_EPI_STORE, L.SD_CONV_WSPLIT if split else 0,
+                       scale.data_ptr() if zs else None, shift.data_ptr() if zs else None, y.data_ptr(), None, s)
+                if zs:
+                    self._zs.add(cl.name)
+            else:
+                L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STORE,
+                       y.data_ptr(), None, 0, None, None, s)
 
-    def _up_fwd(self, u: UpL):
+    def _up_fwd(self, u: UpL, train: bool = True):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         src_cl = self.convs[UP_SRC[u.name] + ".1"]
         Hl, Wl = ws.H >> u.level, ws.W >> u.level
+        if self._use_wsplit(u, train) and dt == L.SD_BF16:
+            # hi/lo split weights: the source twice along K, against [hi | lo] (the generic 1x1 GEMM's two sources)
+            y, bn = t["y:" + src_cl.name], self._bn(src_cl)
+            src = L.make_src(y, src_cl.cout, Hl, Wl, taps=1, bn0=bn, src1=y, c1=src_cl.cout, bn1=bn)
+            L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._ws_ptr(u.off_s), 4 * u.cout, u.kpad_s,
+                   L.SD_EPI_PIXSHUF, t["u:" + u.name].data_ptr(), None, 0, self.params[u.name + ".bias"].data_ptr(),
+                   None, s)
+            return
         src = L.make_src(t["y:" + src_cl.name], src_cl.cout, Hl, Wl, taps=1, bn0=self._bn(src_cl))
         L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(u.off_f), 4 * u.cout, u.kpad_f, L.SD_EPI_PIXSHUF,
                t["u:" + u.name].data_ptr(), None, 0, self.params[u.name + ".bias"].data_ptr(), None, s)
@@ -499,6 +596,11 @@ class UNetEngine:
         """The same conv with the static scales its calibration forward left (sd_conv3x3_q8): one launch."""
         ws, t = self.ws, self.ws.t
         if self._q8_bf16(cl):
+            if self._use_wsplit(cl, False):
+                L.call("sd_conv3x3_ex", self._src_fwd(cl), ws.B, ws.H >> cl.level, ws.W >> cl.level,
+                       self._ws_ptr(cl.off_s), cl.cout, cl.kpad_s, L.SD_EPI_STORE, L.SD_CONV_WSPLIT, None, None,
+                       t["y:" + cl.name].data_ptr(), None, self._s())
+                return
             L.call("sd_conv_gemm", L.SD_BF16, self._src_fwd(cl), ws.B, ws.H >> cl.level, ws.W >> cl.level,
                    self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STORE, t["y:" + cl.name].data_ptr(), None, 0, None,
                    None, self._s())
@@ -513,7 +615,7 @@ class UNetEngine:
         t, s, B, H, W = ws.t, self._s(), ws.B, ws.H, ws.W
         for blk in BLOCKS_FWD:
             if blk in UP_OF_DEC:
-                self._up_fwd(self.ups[UP_OF_DEC[blk]])
+                self._up_fwd(self.ups[UP_OF_DEC[blk]], train=False)
             if blk in PREV_ENC:
                 prev = self.convs[PREV_ENC[blk] + ".1"]
                 lv = prev.level
@@ -535,7 +637,7 @@ class UNetEngine:
         for blk in BLOCKS_FWD:
             if blk in UP_OF_DEC:
                 u = self.ups[UP_OF_DEC[blk]]
-                self._up_fwd(u)  # bf16 ConvTranspose2d (model.py:88-94)
+                self._up_fwd(u, train=False)  # bf16 ConvTranspose2d (model.py:88-94)
                 Pu = B * (H >> (u.level - 1)) * (W >> (u.level - 1))
                 L.call("sd_chan_minmax", t["u:" + u.name].data_ptr(), Pu, u.cout, t["mm:" + u.name].data_ptr(), s)
             if blk in PREV_ENC:
@@ -568,6 +670,8 @@ class UNetEngine:
         self.phase = "fwd"  # read by measurement hooks (bench.py) to tell forward from backward launches
         x = x.contiguous().float()
         L.call("sd_pack_input", self.sd_dtype, x.data_ptr(), B, C, H, W, self.cin_pad0, ws.t["xin"].data_ptr(), self._s())
+        if self.fp8:
+            self._fp8_policy(ws)
         # eval forwards of an unchanged model state (the live app's loop): the launches after the input pack are
         # captured into a HIP graph on the second such forward and replayed from the third on (one host call instead
         # of 27-45 ctypes launches; B=1 960x720 forwards were host-bound at ~20 us of GPU time per kernel)
@@ -575,15 +679,81 @@ class UNetEngine:
         if not train and self.eval_graphs and not self._eval_coeffs and ws.coeff_key is not None:
             gkey = (ws.coeff_key, self._fwd_path(ws))
             if ws.graph is not None and ws.graph_key == gkey:
-                ws.graph.replay()
+                with torch.cuda.device(self.device):  # replays on the current stream of the engine's device
+                    ws.graph.replay()
                 return ws
         self._forward_body(ws, train)
         if gkey is not None and gkey[1] == self._fwd_path(ws):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):  # loader threads may use the device
-                self._forward_body(ws, train)
-            ws.graph, ws.graph_key = g, gkey
+            self._capture(ws, gkey, train)
         return ws
+
+    # ------------------------------------------------------------------ fp8 static-scale recalibration
+    def request_calibration(self):
+        """The next eval forward recomputes the fp8 activation scales from its own input (a calibration forward)."""
+        if self.ws is not None:
+            self.ws.q8_ready = False
+
+    def _fp8_policy(self, ws: Workspace):
+        """Static fp8 scales come from one calibration frame; a later frame with a wider range would saturate at
+        +-448. Two triggers make the next forward a calibration forward again:
+          * range: every static forward compares its packed input's amax with the calibration frame's (one small
+            reduction, the flag copied to pinned host memory without a sync); a frame above `fp8_range_margin` x the
+            calibrated amax triggers recalibration at the following forward (one frame late, no host stall);
+          * age: every `fp8_recalib_every` static forwards (0: never).
+        `fp8_calibrations` counts calibration forwards."""
+        if not (self.fp8_static and self._q8_shapes):
+            return
+        if not ws.q8_ready or self._eval_coeffs:  # this forward calibrates (new state, new workspace, or requested)
+            self.fp8_calibrations += 1
+            self._fp8_age = 0
+            ws.t.pop("cal_amax", None)
+            self._fp8_flag_ev = None
+            return
+        ev = self._fp8_flag_ev
+        if ev is not None and ev.query() and int(self._fp8_flag[0]) != 0:
+            self._fp8_flag[0] = 0
+            self._fp8_flag_ev = None
+            self.fp8_range_recalibrations += 1
+            ws.q8_ready = False
+        elif self.fp8_recalib_every and self._fp8_age >= self.fp8_recalib_every:
+            ws.q8_ready = False
+        if not ws.q8_ready:
+            return self._fp8_policy(ws)
+        self._fp8_age += 1
+        if self.fp8_range_margin > 0:
+            t = ws.t
+            inf = float("inf")
+            if "cal_amax" not in t:  # mm:xin still holds the calibration frame's per-channel (min, max) rows
+                t["cal_amax"] = torch.linalg.vector_norm(t["mm:xin"], ord=inf)
+            cur = torch.linalg.vector_norm(t["xin"], ord=inf).float()  # a max: exact in bf16
+            flag = (cur > self.fp8_range_margin * t["cal_amax"]).to(torch.int32)
+            if self._fp8_flag is None:
+                self._fp8_flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._fp8_flag.copy_(flag.view(1), non_blocking=True)
+            self._fp8_flag_ev = torch.cuda.Event()
+            self._fp8_flag_ev.record(torch.cuda.current_stream(self.device))
+
+    def _capture(self, ws: Workspace, gkey, train: bool):
+        """Capture the forward body into a HIP graph on the engine's OWN capture stream on its device (torch's shared
+        default capture stream lives on whichever device was current at the first capture anywhere in the process;
+        launches on another device's stream would leave the graph empty). Inside the capture, current_stream(device)
+        is that stream, so every launch of the body (L.stream_handle) is recorded."""
+        if getattr(self, "_capture_stream", None) is None:
+            self._capture_stream = torch.cuda.Stream(self.device)
+        g = torch.cuda.CUDAGraph()
+        # outside inference mode: capture_begin advances the CUDA generator's graph-safe state in place, and a state
+        # created by a capture under inference_mode would be an inference tensor that a later capture outside it (a
+        # validation epoch after the live loop) could not update
+        with torch.inference_mode(False), torch.cuda.device(self.device):
+            cur = torch.cuda.current_stream(self.device)
+            self._capture_stream.wait_stream(cur)
+            # thread_local: loader threads may use the device while this thread captures
+            with torch.cuda.graph(g, stream=self._capture_stream, capture_error_mode="thread_local"):
+                if L.stream_handle(self.device) != self._capture_stream.cuda_stream:
+                    raise RuntimeError("eval graph capture: launches would not go to the capture stream")
+                self._forward_body(ws, train)
+            cur.wait_stream(self._capture_stream)
+        ws.graph, ws.graph_key = g, gkey
 
     def _fwd_path(self, ws: Workspace) -> str:
         if not self.fp8:
@@ -592,17 +762,18 @@ class UNetEngine:
 
     def _forward_body(self, ws: Workspace, train: bool):
         B, H, W = ws.B, ws.H, ws.W
+        self._zs = set()  # layers whose stored output is the BN-applied z (eval, zstore)
         if self.fp8:
             return self._forward_fp8(ws)
         for blk in BLOCKS_FWD:
             if blk in UP_OF_DEC:
-                self._up_fwd(self.ups[UP_OF_DEC[blk]])
+                self._up_fwd(self.ups[UP_OF_DEC[blk]], train)
             if blk in PREV_ENC and self.sd_dtype == L.SD_BF16:
                 prev = self.convs[PREV_ENC[blk] + ".1"]
                 lv = prev.level
-                L.call("sd_bnrelu_pool", self.sd_dtype, ws.t["y:" + prev.name].data_ptr(),
-                       ws.t["scale:" + prev.name].data_ptr(), ws.t["shift:" + prev.name].data_ptr(), B, H >> lv,
-                       W >> lv, prev.cout, ws.t["pool:" + prev.name].data_ptr(), self._s())
+                sc, sh = self._bn(prev)
+                L.call("sd_bnrelu_pool", self.sd_dtype, ws.t["y:" + prev.name].data_ptr(), sc.data_ptr(),
+                       sh.data_ptr(), B, H >> lv, W >> lv, prev.cout, ws.t["pool:" + prev.name].data_ptr(), self._s())
             self._conv_fwd(self.convs[blk + ".0"], train)
             self._conv_fwd(self.convs[blk + ".1"], train)
         return ws
@@ -620,8 +791,8 @@ class UNetEngine:
             t["heads_part"] = torch.empty(L.call("sd_heads_rows", P) * (2 * self.c1 + 7), dtype=torch.float32,
                                           device=self.device)
         part = t.get("heads_part")
-        args = (self.sd_dtype, mode, t["y:dec1.1"].data_ptr(), t["scale:dec1.1"].data_ptr(),
-                t["shift:dec1.1"].data_ptr(), P, cl.cout, p["disparity_head.weight"].data_ptr(),
+        hsc, hsh = self._bn(cl)  # identity after a zstore eval forward (y:dec1.1 holds z)
+        args = (self.sd_dtype, mode, t["y:dec1.1"].data_ptr(), hsc.data_ptr(), hsh.data_ptr(), P, cl.cout, p["disparity_head.weight"].data_ptr(),
                 p["disparity_head.bias"].data_ptr(), p["logvar_head.weight"].data_ptr(),
                 p["logvar_head.bias"].data_ptr(), L.ptr(disp), L.ptr(logvar), L.ptr(target), L.ptr(valid),
                 self.count.data_ptr() if mode == L.SD_HEADS_LOSS else None, L.ptr(gdisp), L.ptr(glogvar),
@@ -645,7 +816,7 @@ class UNetEngine:
     def count_valid(self, target: torch.Tensor, valid: torch.Tensor):
         """train.py:329-330 valid count, on device: count_local (this rank's pixels, for the
         metric sums) and count (the loss normaliser; DDP all-reduces it to the global count)."""
-        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self.count_local.data_ptr(), 1,
+        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts.data_ptr(), 2,
                self._s())
 
     # ------------------------------------------------------------------ backward

@@ -221,12 +221,27 @@ class StereoUNet(nn.Module):
         return out
 
     # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def calibrate(self, x: torch.Tensor):
+        """precision="fp8": make this forward a calibration forward (its activations set the static e4m3 scales that
+        the following forwards of this model state reuse). Returns the forward's (disparity, logvar). The engine also
+        recalibrates by itself when a frame's input range outgrows the calibration frame's (UNetEngine._fp8_policy)."""
+        if self.precision == "fp8":
+            self.engine(x.device).request_calibration()
+        return self.forward(x, return_uncertainty=True)
+
     def forward(self, x: torch.Tensor, return_uncertainty: bool = False):
         """model.py:79-104: returns softplus disparity [B,1,H,W] (and clamped logvar).
         precision="fp8" is the inference-only path (eval mode; outputs carry no autograd graph)."""
         eng = self.engine(x.device)
         if self.precision == "fp8" and self.training:
             raise RuntimeError("StereoUNet(precision='fp8') is inference-only (the live app's forward): call .eval()")
+        # launches go to current_stream(eng.device); the guard keeps that device current (a model on cuda:1 while
+        # cuda:0 is current, or engines of several devices in one process)
+        with torch.cuda.device(eng.device):
+            return self._forward(eng, x, return_uncertainty)
+
+    def _forward(self, eng: UNetEngine, x: torch.Tensor, return_uncertainty: bool):
         if (self.precision != "fp8" and torch.is_grad_enabled()
                 and any(p.requires_grad for p in self.parameters())):
             disp, logvar = _UNetFunction.apply(self, x, *[p for _, p in self._named_trainable()])

@@ -51,6 +51,11 @@ def train_step(model: StereoUNet, optimizer: FusedAdamW | None, inputs, targets,
     (an async collective), the handle is waited on after the forward, which the collective then overlaps.
     """
     eng = model.engine(inputs.device)
+    with torch.cuda.device(eng.device):
+        _train_step(model, eng, optimizer, inputs, targets, valid_mask, grad_hook, count_hook, before_step)
+
+
+def _train_step(model, eng, optimizer, inputs, targets, valid_mask, grad_hook, count_hook, before_step):
     training = optimizer is not None
     mask_u8 = valid_mask.contiguous().view(torch.uint8)
     targets = targets.contiguous()

@@ -233,10 +233,108 @@ def gen_bf16():
     np.savez_compressed(OUT / "full_bf16.npz", **out)
 
 
+TRAINED_STEPS, TRAINED_B, TRAINED_LR = 600, 4, 5e-3
+# held-out evaluation sets of the trained checkpoint: (name, batches, batch size, H, W, first seed of synthetic_batch on
+# the CPU, batches whose output maps are stored); EPE over all batches (the validation epoch's mean)
+TRAINED_EVAL = (("val240", 4, 4, 240, 320, 90_001, 1), ("val720", 2, 1, 720, 960, 90_101, 1))
+
+
+def _synthetic(batch, h, w, seed):
+    from stereo_depth_estimation_amd.data import synthetic_batch
+
+    return {k: v.numpy() for k, v in synthetic_batch(batch, h, w, seed=seed).items()}
+
+
+def _input_digest(b):
+    """sha256 of a synthetic batch's bytes: the GPU box regenerates the batch from its seed and checks this before
+    trusting the stored outputs (same torch CPU generator and kernels, same image)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for k in ("input", "target", "valid_mask"):
+        h.update(np.ascontiguousarray(b[k]).tobytes())
+    return np.array(h.hexdigest())
+
+
+def gen_trained():
+    """A reference-TRAINED base-32 checkpoint: the reference's own run_epoch (train.py:292-418)
+    with its AdamW (train.py:578, --lr 5e-3) trains StereoUNet from the make_state(seed=3) weights for TRAINED_STEPS
+    steps on fresh synthetic rectified pairs (stereo_depth_estimation_amd.data.synthetic_batch, the bench's SURVEY
+    §8d recipe) at 240x320, batch TRAINED_B. Written: the state_dict (trained_state.npz) and, per held-out set of
+    TRAINED_EVAL, the reference's eval-mode validation (train.py:301: eval BN, no optimizer) in fp32 and under
+    torch.autocast("cpu", bfloat16): metrics (EPE = `mae`, train.py:350,406), disparity and logvar maps, and the
+    input checksums (trained_eval.npz). ~4 min on 8 cores."""
+    import time
+
+    base = 32
+    m = build_ref(base, make_state(base, seed=3)).train()
+    names = trainable_named(m)
+    opt = torch.optim.AdamW([p for _, p in names], lr=TRAINED_LR, weight_decay=1e-4)
+    t0 = time.time()
+    for i in range(TRAINED_STEPS):
+        b = batch_to_torch(_synthetic(TRAINED_B, 240, 320, seed=60_000 + i))
+        metrics, _ = ref_train.run_epoch(m, [b], torch.device("cpu"), optimizer=opt, global_step=i)
+        if i % 50 == 0 or i == TRAINED_STEPS - 1:
+            print(f"step {i}: mae {metrics['mae']:.3f} nll {metrics['nll']:.3f} ({time.time() - t0:.0f}s)", flush=True)
+    sd = m.state_dict()
+    np.savez_compressed(OUT / "trained_state.npz", **{k: v.numpy() for k, v in sd.items()})
+    out = {"train/steps": np.int64(TRAINED_STEPS), "train/batch": np.int64(TRAINED_B), "train/lr": np.float64(TRAINED_LR)}
+    for name, nb, bsz, h, w, seed, nmaps in TRAINED_EVAL:
+        bs = [_synthetic(bsz, h, w, seed + i) for i in range(nb)]
+        out[f"{name}/seed"], out[f"{name}/shape"] = np.int64(seed), np.array([nb, bsz, h, w])
+        out[f"{name}/digest"] = np.array([_input_digest(b) for b in bs])
+        for tag, ac in (("fp32", False), ("bf16", True)):
+            me = copy.deepcopy(m).eval()
+            with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16, enabled=ac):
+                for i in range(nmaps):
+                    d, lv = me(torch.as_tensor(bs[i]["input"]), return_uncertainty=True)
+                    out[f"{name}/{tag}/disp{i}"], out[f"{name}/{tag}/logvar{i}"] = d.float().numpy(), lv.float().numpy()
+                vm, _ = ref_train.run_epoch(me, [batch_to_torch(b) for b in bs], torch.device("cpu"), optimizer=None)
+            for k, v in vm.items():
+                out[f"{name}/{tag}/metrics/{k}"] = np.float64(v)
+            print(f"{name} {tag}: {vm}", flush=True)
+    np.savez_compressed(OUT / "trained_eval.npz", **out)
+
+
+# BASELINE configs' per-GPU train steps (VERDICT r03 item 3): (name, batch, H, W, synthetic_batch seed)
+CONFIG_STEPS = (("c2", 64, 240, 320, 21), ("c4", 16, 480, 640, 22))
+
+
+def gen_configs():
+    """One reference train step (run_epoch, train.py:292-418, AdamW lr 1e-3) at BASELINE config 2's per-GPU batch
+    (64 x 320x240) and config 4's (16 x 640x480), from make_state(32, seed=3), in fp32 and under
+    torch.autocast("cpu", bfloat16): metrics and per-tensor gradient norms / sums, plus the input digest
+    (configs_steps.npz). ~15 GB of host memory per step."""
+    import time
+
+    out = {}
+    state = make_state(32, seed=3)
+    for name, bsz, h, w, seed in CONFIG_STEPS:
+        b = _synthetic(bsz, h, w, seed)
+        out[f"{name}/seed"], out[f"{name}/shape"] = np.int64(seed), np.array([bsz, h, w])
+        out[f"{name}/digest"] = _input_digest(b)
+        for tag, ac in (("fp32", False), ("bf16", True)):
+            t0 = time.time()
+            m = build_ref(32, state)
+            names = trainable_named(m)
+            opt = RecordingAdamW([p for _, p in names], names, lr=1e-3, weight_decay=1e-4)
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=ac):
+                metrics, _ = ref_train.run_epoch(m, [batch_to_torch(b)], torch.device("cpu"), optimizer=opt)
+            for k, v in metrics.items():
+                out[f"{name}/{tag}/metrics/{k}"] = np.float64(v)
+            for k, g in opt.grads[0].items():
+                out[f"{name}/{tag}/gnorm/{k}"] = np.float64(g.double().norm().item())
+                out[f"{name}/{tag}/gsum/{k}"] = np.float64(g.double().sum().item())
+            print(f"{name} {tag}: {metrics} ({time.time() - t0:.0f}s)", flush=True)
+            del m, opt
+    np.savez_compressed(OUT / "configs_steps.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     parts = sys.argv[1:] or ["data", "tiny", "full", "bf16"]
     for part in parts:
-        {"data": gen_data, "tiny": gen_tiny, "full": gen_full, "bf16": gen_bf16}[part]()
+        {"data": gen_data, "tiny": gen_tiny, "full": gen_full, "bf16": gen_bf16, "trained": gen_trained,
+         "configs": gen_configs}[part]()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)

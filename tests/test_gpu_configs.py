@@ -218,43 +218,167 @@ def test_c2_batch64_train_step_bf16_vs_oracle_and_fp32(golden_dir):
     assert max(e.values()) <= max(ac_g.values()), max(e.items(), key=lambda kv: kv[1])
 
 
-# ---------------------------------------------------------------------------------------------- EPE, trained model
-def test_epe_bf16_and_fp32_vs_oracle_on_trained_checkpoint():
-    """North star: "disparity EPE within 1e-3 of reference". EPE is the reference's `mae` (train.py:350,406): mean
-    |disparity - target| over valid pixels in the validation epoch (eval-mode BN, train.py:301). A bf16 model is
-    trained on synthetic rectified pairs until its disparity tracks the targets; then the same checkpoint is
-    evaluated on held-out pairs by the bf16 path, the fp32 path and the CPU oracle (the reference's arithmetic), in
-    fp32 and under torch.autocast(bf16). Bounds: |EPE_fp32 - EPE_ref| < 1e-5 px (the north star's 1e-3, met with
-    room: measured 0 at 6 decimals); |EPE_bf16 - EPE_ref| below the north star's 1e-3 px or 2x the reference's own
-    autocast(bf16) EPE shift, whichever is larger. bf16 does NOT meet 1e-3 on a trained model, for the reference
-    either: bf16-rounded weights perturb the function systematically (measured on 4 pairs at EPE 5.27 px: HIP bf16
-    6.9e-3, reference autocast 4.4e-3; bench.py reports the same gap at B=128 as `epe`). (Training uses lr 5e-3 so
-    that 400 steps reach the targets' scale; the optimizer is not what is tested here.)"""
+# ---------------------------------------------------------------------------------------------- per-GPU config steps
+@pytest.mark.parametrize("name", ["c2", "c4"])
+def test_config_batch_train_step_vs_reference_fixture(golden_dir, name):
+    """BASELINE config 2's per-GPU step (64 pairs at 320x240, the bench's workload) and config 4's (16 pairs at
+    640x480): one train step from make_state(32, seed=3) against the REFERENCE's own step on the same batch
+    (configs_steps.npz, gen_golden.py gen_configs: fp32 and torch.autocast(bf16) on the CPU). These shapes take the
+    kernels' large-batch paths (split-K counts, slab sizes, persistent-grid item counts) that B=2 never reaches.
+      fp32 HIP: loss metrics to 1e-5, per-tensor gradient norms to 5e-3 (the full-size bounds of test_gpu_model)
+      bf16 HIP: loss metrics within the reference autocast's own metric drift (floor 1e-6); gradient norms: median
+                and worst-tensor relative error <= 1.5x the reference autocast's (test module docstring)"""
+    from stereo_depth_estimation_amd.data import synthetic_batch
+
+    g = np.load(golden_dir / "configs_steps.npz")
+    bsz, h, w = (int(v) for v in g[f"{name}/shape"])
+    b = synthetic_batch(bsz, h, w, seed=int(g[f"{name}/seed"]))
+    assert _input_digest(b) == str(g[f"{name}/digest"]), "regenerated inputs differ from the reference run's"
+    b = {k: v.numpy() for k, v in b.items()}
+
+    def fix(tag):
+        return ({k.split("/")[-1]: float(g[k]) for k in g.files if k.startswith(f"{name}/{tag}/metrics/")},
+                {k[len(f"{name}/{tag}/gnorm/"):]: float(g[k]) for k in g.files if k.startswith(f"{name}/{tag}/gnorm/")})
+
+    ref, ac = fix("fp32"), fix("bf16")
+    st = U.make_state(32, seed=3)
+    m32, g32 = _hip_step(st, "fp32", b)
+    for k, v in ref[0].items():
+        assert abs(m32[k] - v) <= 1e-5 * abs(v), ("fp32", k, m32[k], v)
+    worst = max(ref[1], key=lambda k: abs(g32[k] - ref[1][k]) / ref[1][k])
+    print(f"{name}: fp32 worst grad-norm rel err {abs(g32[worst] - ref[1][worst]) / ref[1][worst]:.2e} ({worst})")
+    for k, v in ref[1].items():
+        assert abs(g32[k] - v) <= 5e-3 * v + 1e-7, ("fp32", k, g32[k], v)
+    got = _hip_step(st, "bf16", b)
+    em, am = _rel(got[0], ref[0]), _rel(ac[0], ref[0])
+    eg, ag = _rel(got[1], ref[1]), _rel(ac[1], ref[1])
+    print(f"{name}: bf16 metric rel err {em}, autocast {am}; grad-norm rel err median {np.median(list(eg.values())):.2e} "
+          f"worst {max(eg.values()):.2e}, autocast median {np.median(list(ag.values())):.2e} worst {max(ag.values()):.2e}")
+    _assert_step_within(got, ref, ac)
+
+
+# ---------------------------------------------------------------------------------------------- EPE, trained models
+def _input_digest(b):
+    import hashlib
+
+    h = hashlib.sha256()
+    for k in ("input", "target", "valid_mask"):
+        h.update(np.ascontiguousarray(b[k].numpy()).tobytes())
+    return h.hexdigest()
+
+
+def _val_set(ev, name):
+    """The held-out set of trained_eval.npz, regenerated from its seeds on the CPU and checked against the digests the
+    reference run recorded (gen_golden.py gen_trained)."""
+    from stereo_depth_estimation_amd.data import synthetic_batch
+
+    nb, bsz, h, w = (int(v) for v in ev[f"{name}/shape"])
+    seed = int(ev[f"{name}/seed"])
+    bs = [synthetic_batch(bsz, h, w, seed=seed + i) for i in range(nb)]
+    for i, b in enumerate(bs):
+        assert _input_digest(b) == str(ev[f"{name}/digest"][i]), f"{name} batch {i}: regenerated inputs differ"
+    return bs
+
+
+def _hip_epe(model, bs):
+    from stereo_depth_estimation_amd.train import run_epoch
+
+    return run_epoch(model, [{k: v.to(DEV) for k, v in b.items()} for b in bs], torch.device(DEV))[0]
+
+
+@pytest.mark.parametrize("name", ["val240", "val720"])
+def test_epe_on_reference_trained_checkpoint(golden_dir, name):
+    """North star: "disparity EPE within 1e-3 of reference" (EPE = the reference's `mae`, train.py:350,406, over the
+    validation epoch in eval BN, train.py:301). The checkpoint was trained BY THE REFERENCE on the CPU (600 steps at
+    240x320, gen_golden.py gen_trained); its fp32 and autocast(bf16) validation metrics and maps are the reference's own.
+    val240 (16 held-out pairs at the training resolution, EPE 4.69 px):
+      fp32 HIP : per-pixel |Δ| < 1e-3 on disparity and logvar, |ΔEPE| < 1e-5 px
+      bf16 HIP : |ΔEPE| < 1e-3 px, strict. The eval forward takes every weight as a hi/lo bf16 pair and stores the
+                 BN-applied activations (sd_conv3x3_ex); before that the shift was ~1e-2 px, the reference's own
+                 autocast shifts it by 7e-3 px (tools/precision_study.py)
+      fp8 HIP  : |ΔEPE| <= 1 % of the EPE and mean per-pixel |Δ| <= 1 % of the mean disparity (e4m3 keeps 3 mantissa
+                 bits: the live path's speed mode, measured 0.7 % / 0.5 %; it does not meet 1e-3)
+    val720 (2 pairs at 960x720, 3x the trained disparities, EPE ~40 px: the model is off its training distribution, its
+    errors are one-signed and an EPE shift equals the mean output shift, so EPE is not the yardstick there):
+      fp32 per-pixel and EPE as above; bf16 mean per-pixel |Δ| <= the reference autocast's; fp8 as at val240"""
+    from stereo_depth_estimation_amd.model import StereoUNet
+
+    st = dict(np.load(golden_dir / "trained_state.npz"))
+    ev = np.load(golden_dir / "trained_eval.npz")
+    bs = _val_set(ev, name)
+    ref = {k: float(ev[f"{name}/fp32/metrics/{k}"]) for k in ("mae", "nll", "rmse", "sigma")}
+    ac = {k: float(ev[f"{name}/bf16/metrics/{k}"]) for k in ("mae", "nll", "rmse", "sigma")}
+    out, epe = {}, {}
+    for prec in ("fp32", "bf16", "fp8"):
+        m = StereoUNet(precision=prec)
+        m.load_state_dict({k: torch.as_tensor(v) for k, v in st.items()})
+        m = m.to(DEV)
+        if prec != "fp8":
+            epe[prec] = _hip_epe(m, bs)
+        m.eval()
+        with torch.inference_mode():
+            x = bs[0]["input"].to(DEV)
+            if prec == "fp8":  # calibration forward, then the static (live-loop) forward the bound is for
+                m(x)
+                mae_sum, n = 0.0, 0
+                for b in bs:
+                    d = m(b["input"].to(DEV)).cpu()
+                    msk = b["valid_mask"] & torch.isfinite(b["target"])
+                    mae_sum += float((d[msk].double() - b["target"][msk].double()).abs().sum())
+                    n += int(msk.sum())
+                epe[prec] = {"mae": mae_sum / n}
+            out[prec] = [t.cpu() for t in m(x, return_uncertainty=True)]
+    d_ref = torch.as_tensor(ev[f"{name}/fp32/disp0"])
+    lv_ref = torch.as_tensor(ev[f"{name}/fp32/logvar0"])
+    d_ac = torch.as_tensor(ev[f"{name}/bf16/disp0"])
+    per = {p: float((out[p][0] - d_ref).abs().mean()) for p in out}
+    print(f"{name}: EPE ref {ref['mae']:.6f} | fp32 {epe['fp32']['mae'] - ref['mae']:+.2e} bf16 "
+          f"{epe['bf16']['mae'] - ref['mae']:+.2e} fp8 {epe['fp8']['mae'] - ref['mae']:+.2e} ref-autocast "
+          f"{ac['mae'] - ref['mae']:+.2e} | mean |d| per pixel: {per}, ref-autocast "
+          f"{float((d_ac - d_ref).abs().mean()):.3g}")
+    assert float((out["fp32"][0] - d_ref).abs().max()) < 1e-3
+    assert float((out["fp32"][1] - lv_ref).abs().max()) < 1e-3
+    for k in ref:
+        assert abs(epe["fp32"][k] - ref[k]) < 1e-5 * max(1.0, abs(ref[k])), (k, epe["fp32"][k], ref[k])
+    mean_disp = float(d_ref.abs().mean())
+    assert per["fp8"] <= 0.01 * mean_disp, (per, mean_disp)
+    if name == "val240":
+        assert abs(epe["bf16"]["mae"] - ref["mae"]) < 1e-3, (epe["bf16"]["mae"], ref["mae"])
+        assert abs(epe["fp8"]["mae"] - ref["mae"]) <= 0.01 * ref["mae"], (epe["fp8"]["mae"], ref["mae"])
+    else:
+        assert per["bf16"] <= float((d_ac - d_ref).abs().mean()), per
+
+
+@pytest.mark.parametrize("seed", [42, 7])
+def test_epe_bf16_and_fp32_on_models_trained_in_test(seed):
+    """The same bound on two more checkpoints, trained here by the bf16 HIP path (400 steps at B=32 on synthetic pairs,
+    lr 5e-3 so that they reach the targets' scale; the optimizer is not what is tested): over 16 held-out pairs
+    |EPE_bf16 - EPE_fp32| < 1e-3 px, the fp32 path's EPE equal to the CPU oracle's (the reference's arithmetic) to 1e-5
+    px on the first 4 of them."""
     from stereo_depth_estimation_amd.data import synthetic_batch
     from stereo_depth_estimation_amd.model import StereoUNet
     from stereo_depth_estimation_amd.optim import FusedAdamW
     from stereo_depth_estimation_amd.train import run_epoch, train_step
 
-    torch.manual_seed(42)
+    torch.manual_seed(seed)
     m = StereoUNet(precision="bf16").to(DEV).train()
     opt = FusedAdamW(m.parameters(), lr=5e-3, weight_decay=1e-4)
-    train = [synthetic_batch(32, 240, 320, seed=700 + i, device=DEV) for i in range(8)]
-    val = synthetic_batch(16, 240, 320, seed=999, device=DEV)
-    e0 = run_epoch(m, [val], torch.device(DEV))[0]["mae"]
+    train = [synthetic_batch(32, 240, 320, seed=700 + 37 * seed + i, device=DEV) for i in range(8)]
+    val = [synthetic_batch(4, 240, 320, seed=9_000 + 53 * seed + i) for i in range(4)]
+    e0 = _hip_epe(m, val)["mae"]
     m.train()
     for i in range(400):
         b = train[i % len(train)]
         train_step(m, opt, b["input"], b["target"], b["valid_mask"])
-    e16 = run_epoch(m, [val], torch.device(DEV))[0]["mae"]
+    e16 = _hip_epe(m, val)["mae"]
     m32 = StereoUNet(precision="fp32").to(DEV)
     m32.load_state_dict(m.state_dict())
-    e32 = run_epoch(m32, [val], torch.device(DEV))[0]["mae"]
+    e32 = _hip_epe(m32, val)["mae"]
+    e32_first = _hip_epe(m32, val[:1])["mae"]
     sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
-    vb = [{k: v.cpu().numpy() for k, v in val.items()}]
-    ref, _ = U.run_epoch(U.Net(sd), vb, None)
-    with torch.autocast("cpu", dtype=torch.bfloat16):
-        ac, _ = U.run_epoch(U.Net(sd), vb, None)
-    print(f"EPE: init {e0:.4f}, bf16 {e16:.6f}, fp32 {e32:.6f}, oracle {ref['mae']:.6f}, oracle autocast {ac['mae']:.6f}")
+    o, _ = U.run_epoch(U.Net(sd), [{k: v.numpy() for k, v in val[0].items()}], None)
+    print(f"seed {seed}: EPE init {e0:.4f}, fp32 {e32:.6f}, bf16 {e16:.6f} ({e16 - e32:+.2e}), oracle (4 pairs) "
+          f"{o['mae']:.6f} vs fp32 {e32_first:.6f}")
     assert e16 < 0.5 * e0, ("the model did not train", e0, e16)
-    assert abs(e32 - ref["mae"]) < 1e-5, (e32, ref["mae"])
-    assert abs(e16 - ref["mae"]) < max(1e-3, 2 * abs(ac["mae"] - ref["mae"])), (e16, ref["mae"], ac["mae"])
+    assert abs(e32_first - o["mae"]) < 1e-5, (e32_first, o["mae"])
+    assert abs(e16 - e32) < 1e-3, (e16, e32)

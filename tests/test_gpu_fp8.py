@@ -261,3 +261,47 @@ def test_fp8_static_scales_on_other_frames():
             d_dyn = m(x.to(DEV))
             eng.fp8_static = True
             assert float((d - d_dyn).abs().mean()) <= 0.02 * float(d_dyn.abs().mean())
+
+
+def test_fp8_recalibrates_when_the_input_range_grows():
+    """scales calibrated on a low-contrast startup frame must not stay in force for a full-range frame.
+    The static forward's input-range check flags the wider frame; the next forward recalibrates and is back within
+    the fp8 bound of the fp32 reference. Frames of the calibration frame's range trigger nothing; calibrate(x) and the
+    age policy force a calibration forward."""
+    from stereo_depth_estimation_amd.model import StereoUNet
+
+    st = U.make_state(32, seed=5)
+    m = StereoUNet(base_channels=32, precision="fp8")
+    m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in st.items()})
+    m = m.to(DEV).eval()
+    eng = m.engine()
+    net = U.Net(st, base_channels=32)
+    bright = torch.as_tensor(U.make_batch(1, 240, 320, seed=33)["input"])
+    dark = 0.2 * torch.as_tensor(U.make_batch(1, 240, 320, seed=34)["input"])
+    with torch.no_grad():
+        d_ref, _ = net.forward(bright, train=False)
+    with torch.inference_mode():
+        m(dark.to(DEV))  # calibration on the dark frame
+        assert eng.fp8_calibrations == 1
+        for _ in range(2):  # same range: static forwards, no trigger
+            m(0.2 * torch.as_tensor(U.make_batch(1, 240, 320, seed=35)["input"]).to(DEV))
+        torch.cuda.synchronize()
+        assert eng.fp8_calibrations == 1 and eng.fp8_range_recalibrations == 0
+        d_stale = m(bright.to(DEV))  # static forward with the dark frame's scales: flagged
+        torch.cuda.synchronize()
+        d_new = m(bright.to(DEV))  # recalibrates on the bright frame
+        assert eng.fp8_range_recalibrations == 1 and eng.fp8_calibrations == 2
+        d_next = m(bright.to(DEV))  # static again, with the bright frame's scales
+        torch.cuda.synchronize()
+        assert eng.fp8_calibrations == 2
+    err = {k: float((v.cpu() - d_ref).abs().mean()) / float(d_ref.abs().mean())
+           for k, v in (("stale", d_stale), ("recalibrated", d_new), ("static", d_next))}
+    print("fp8 mean rel err vs fp32:", err)
+    assert err["recalibrated"] <= FP8_MEAN_REL and err["static"] <= FP8_MEAN_REL, err
+    with torch.inference_mode():
+        m.calibrate(bright.to(DEV))
+        assert eng.fp8_calibrations == 3
+        eng.fp8_recalib_every = 2
+        for _ in range(3):
+            m(bright.to(DEV))
+        assert eng.fp8_calibrations == 4  # the age policy: after 2 static forwards

@@ -347,3 +347,30 @@ def test_640x480_forward_fp32_and_bf16_vs_oracle():
         err, drift = (got - ref).abs(), (ac - ref).abs()
         assert float(err.max()) <= 1.5 * float(drift.max()), (float(err.max()), float(drift.max()))
         assert float(err.mean()) <= 1.5 * float(drift.mean()), (float(err.mean()), float(drift.mean()))
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_eval_graph_replays_new_inputs(precision):
+    """Eval forwards of an unchanged state: the 2nd captures a HIP graph on the engine's own capture stream, the 3rd
+    replays it. Each forward's output must be that input's eager output (an empty or stale graph would return the
+    previous frame's outputs), also when the caller runs the forwards on a side stream."""
+    st = U.make_state(8, seed=2, signed_gamma=True)
+    m = _hip_model(st, 8, precision).eval()
+    ref = _hip_model(st, 8, precision).eval()
+    ref.engine().eval_graphs = False
+    xs = [torch.as_tensor(U.make_batch(1, 32, 48, seed=s)["input"]).to(DEV) for s in (40, 41, 42, 43)]
+    side = torch.cuda.Stream()
+    with torch.inference_mode():
+        ref(xs[0])  # fp8: the same calibration frame for both models
+        m(xs[0])
+        for i, x in enumerate(xs[1:]):
+            if i == 1:
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    d, lv = m(x, return_uncertainty=True)
+                torch.cuda.current_stream().wait_stream(side)
+            else:
+                d, lv = m(x, return_uncertainty=True)
+            de, lve = ref(x, return_uncertainty=True)
+            assert torch.equal(d, de) and torch.equal(lv, lve), (precision, i)
+    assert m.engine().ws.graph is not None

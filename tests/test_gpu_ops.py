@@ -663,3 +663,127 @@ def test_conv3x3_wgrad_dual_source_spanning_block(B, H, W, c0, c1, co, fused):
     assert float((dw.cpu() - ref).abs().max()) <= 2e-2 * (1 + float(ref.abs().max()))
     if fused:
         assert not torch.isnan(_from_nhwc(dyd, B, H, W, co)).any()
+
+
+# ---------------------------------------------------------------------------------------------- hi/lo split weights
+def _pack_split(w, ci_pad):
+    """SD_PACK_CONV3_FWD_SPLIT through sd_pack_weights: [co][kpad], k = tap*2*ci_pad + {hi ci | ci_pad + lo ci}."""
+    lib = L()
+    co, ci = w.shape[:2]
+    kpad = ((18 * ci_pad + 63) // 64) * 64
+    out = torch.empty(co * kpad, dtype=torch.bfloat16, device=DEV)
+    wd = w.contiguous().to(DEV)
+    job = (lib.SdPackJob * 1)(lib.SdPackJob(wd.data_ptr(), lib.SD_PACK_CONV3_FWD_SPLIT, co, ci, ci_pad, kpad, 0))
+    lib.call("sd_pack_weights", lib.SD_BF16, job, 1, out.data_ptr(), lib.stream_handle())
+    torch.cuda.synchronize()
+    return out, kpad, wd
+
+
+def test_pack_conv3_split_is_hi_plus_lo():
+    torch.manual_seed(7)
+    w = torch.randn(32, 24, 3, 3) / 7
+    out, kpad, _ = _pack_split(w, 32)
+    p = out.float().cpu().reshape(32, kpad)[:, :9 * 64].reshape(32, 9, 2, 32)
+    hi, lo = p[:, :, 0, :24], p[:, :, 1, :24]
+    ref = w.permute(0, 2, 3, 1).reshape(32, 9, 24)
+    assert torch.equal(hi, ref.to(torch.bfloat16).float())  # hi = RNE(w)
+    assert float(((hi + lo) - ref).abs().max()) <= 2.0 ** -16 * float(ref.abs().max())
+    assert float(p[:, :, :, 24:].abs().max()) == 0.0  # channel padding stays zero
+    assert float(out.float().cpu().reshape(32, kpad)[:, 9 * 64:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("B,H,W,c0,c1,co,bn,epi", [
+    (2, 32, 64, 8, 0, 32, False, "stats"),   # enc1.0: the 8-channel input, CK = 8 chunks
+    (2, 30, 50, 8, 0, 32, False, "affine"),  # ragged tiles, BN affine epilogue (CK = 8, 32x32 MFMA epilogue)
+    (1, 32, 64, 32, 0, 32, True, "store"),   # enc1.1 / dec1.1: 32 -> 32 with BN+ReLU, 16x32 tiles
+    (1, 32, 64, 32, 32, 32, True, "stats"),  # dec1.0: cat([up, skip]) (two sources, four chunks)
+    (1, 32, 64, 32, 32, 32, True, "affine"),
+    (2, 15, 20, 64, 0, 64, True, "store"),   # N % 64 shapes: whole-image tiles, NT = 2, RT = 2 / 3
+    (2, 15, 20, 64, 64, 128, True, "affine"),
+    (1, 30, 40, 128, 0, 128, True, "affine"),
+])
+def test_conv3x3_ex_split_weights_and_affine_epilogue(B, H, W, c0, c1, co, bn, epi):
+    """sd_conv3x3_ex(SD_CONV_WSPLIT): the product of the bf16 operand with the fp32 weights (hi + lo), to within one bf16
+    rounding of the output, where the plain bf16 conv carries the weights' bf16 rounding (~2^-9); BN statistics of the
+    stored values as sd_conv_gemm. "affine": the eval BatchNorm in the epilogue, out = bf16(acc*scale + shift)."""
+    lib = L()
+    torch.manual_seed(3)
+    ci = c0 + c1
+    u = torch.randn(B, c0, H, W).to(torch.bfloat16).float() + (0.5 if not bn else 0.0)
+    s = torch.randn(B, c1, H, W).to(torch.bfloat16).float() if c1 else None
+    sc, sh = torch.rand(ci) + 0.5, torch.randn(ci) * 0.2
+    w = torch.randn(co, ci, 3, 3) / (3 * ci ** 0.5)
+    if c1:  # dec1.0 form: the up part raw, the skip part BN+ReLU
+        xs = torch.relu(s * sc[None, c0:, None, None] + sh[None, c0:, None, None]).to(torch.bfloat16).float()
+        x = torch.cat([u, xs], 1)
+    elif bn:
+        x = torch.relu(u * sc[None, :, None, None] + sh[None, :, None, None]).to(torch.bfloat16).float()
+    else:
+        x = u
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    wp, kpad, _ = _pack_split(w, ci)
+    ud = _nhwc(u, "bf16")
+    if c1:
+        src = lib.make_src(ud, c0, H, W, taps=9, src1=_nhwc(s, "bf16"), c1=c1,
+                           bn1=(sc[c0:].contiguous().to(DEV), sh[c0:].contiguous().to(DEV)))
+    else:
+        src = lib.make_src(ud, c0, H, W, taps=9, bn0=(sc.to(DEV), sh.to(DEV)) if bn else None)
+    assert lib.call("sd_conv3x3_ex_ok", src, co) == 1
+    out = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=DEV)
+    e = lib.SD_EPI_STATS if epi == "stats" else lib.SD_EPI_STORE
+    rows = lib.call("sd_conv_gemm_stat_rows", lib.SD_BF16, B, H, W, co)
+    stats = torch.zeros(rows, co, 2, device=DEV)
+    osc, osh = torch.rand(co) + 0.5, torch.randn(co)
+    osc[::5] *= -1
+    aff = (osc.to(DEV), osh.to(DEV)) if epi == "affine" else (None, None)
+    lib.call("sd_conv3x3_ex", src, B, H, W, wp.data_ptr(), co, kpad, e, lib.SD_CONV_WSPLIT, lib.ptr(aff[0]),
+             lib.ptr(aff[1]), out.data_ptr(), stats.data_ptr() if e == lib.SD_EPI_STATS else None, lib.stream_handle())
+    got = _from_nhwc(out, B, H, W, co).double()
+    if epi == "affine":  # the stored value is the BN-applied z; compare z, and take y back out for the checks below
+        ref = ref * osc.double()[None, :, None, None] + osh.double()[None, :, None, None]
+        err = float((got - ref.float().to(torch.bfloat16).double()).abs().max())
+        assert err <= 2.0 ** -7 * float(ref.abs().max()), err  # at most one bf16 ulp apart after rounding
+        return
+    # the output is stored bf16: compare the pre-rounding error through the rounding of the reference
+    err = float((got - ref.float().to(torch.bfloat16).double()).abs().max())
+    assert err <= 2.0 ** -7 * float(ref.abs().max()), err  # at most one bf16 ulp apart after rounding
+    # the plain bf16 conv (weights rounded) vs the split one: mean error to the fp64 reference, before output rounding
+    wq = w.to(torch.bfloat16).double()
+    e_plain = float((F.conv2d(x.double(), wq, padding=1) - ref).abs().mean())
+    e_split = float((got - ref).abs().mean())
+    print(f"mean |err|: split (incl. bf16 output rounding) {e_split:.3g}, bf16 weights (before rounding) {e_plain:.3g}")
+    if e == lib.SD_EPI_STATS:
+        st = stats.double().sum(0).cpu()
+        assert torch.allclose(st[:, 0], got.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    # name of the launched instance (rocprofv3): the chunks run twice, so one-chunk layers keep their weights in LDS
+    name = L().kernel_name("sd_conv3x3_ex_kernel_name", src, H, W, co, e, lib.SD_CONV_WSPLIT, 0)
+    assert name.startswith("k_halo_conv<")
+
+
+def test_convT_split_pack_doubled_k_matches_fp32_weights():
+    """up1's hi/lo forward: the source twice along K (two sources of the 1x1 GEMM) against SD_PACK_CONVT_FWD_SPLIT
+    rows [hi | lo]: ConvTranspose2d with the fp32 weights (bias, pixel shuffle) to one bf16 ulp of the output."""
+    lib = L()
+    torch.manual_seed(5)
+    B, H, W, ci, co = 2, 12, 20, 64, 32
+    y = torch.randn(B, ci, H, W).to(torch.bfloat16).float()
+    sc, sh = torch.rand(ci) + 0.5, torch.randn(ci) * 0.2
+    w = torch.randn(ci, co, 2, 2) / 8
+    bias = torch.randn(co) * 0.1
+    x = torch.relu(y * sc[None, :, None, None] + sh[None, :, None, None]).to(torch.bfloat16).float()
+    ref = F.conv_transpose2d(x.double(), w.double(), bias.double(), stride=2)
+    kpad = ((2 * ci + 63) // 64) * 64
+    wp = torch.empty(4 * co * kpad, dtype=torch.bfloat16, device=DEV)
+    wd = w.contiguous().to(DEV)
+    job = (lib.SdPackJob * 1)(lib.SdPackJob(wd.data_ptr(), lib.SD_PACK_CONVT_FWD_SPLIT, co, ci, ci, kpad, 0))
+    lib.call("sd_pack_weights", lib.SD_BF16, job, 1, wp.data_ptr(), lib.stream_handle())
+    yd = _nhwc(y, "bf16")
+    bn = (sc.to(DEV), sh.to(DEV))
+    src = lib.make_src(yd, ci, H, W, taps=1, bn0=bn, src1=yd, c1=ci, bn1=bn)
+    out = torch.empty(B * 4 * H * W, co, dtype=torch.bfloat16, device=DEV)
+    bd = bias.to(DEV)
+    lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), 4 * co, kpad, lib.SD_EPI_PIXSHUF,
+             out.data_ptr(), None, 0, bd.data_ptr(), None, lib.stream_handle())
+    got = _from_nhwc(out, B, 2 * H, 2 * W, co).double()
+    err = float((got - ref.float().to(torch.bfloat16).double()).abs().max())
+    assert err <= 2.0 ** -7 * float(ref.abs().max()), err
