@@ -282,10 +282,12 @@ def infer_fp8(torch, model, dev, H=720, W=960, iters=20):
     sd = model.state_dict()
     x = synthetic_batch(1, H, W, seed=5, device=dev)["input"]
     out, ms = {}, {}
-    for prec in ("fp8", "bf16", "fp32"):
-        m = StereoUNet(precision=prec)
+    for prec in ("fp8", "bf16", "bf16_fast", "fp32"):
+        m = StereoUNet(precision=prec.split("_")[0])
         m.load_state_dict({k: v.detach().cpu() for k, v in sd.items()})
         m = m.to(dev).eval()
+        if prec == "bf16_fast":  # plain bf16 weights in the eval forward (sd_conv3x3_ex's hi/lo pairs off)
+            m.engine().wsplit_eval = False
         with torch.inference_mode():
             for _ in range(3):
                 m(x, return_uncertainty=True)
@@ -301,7 +303,10 @@ def infer_fp8(torch, model, dev, H=720, W=960, iters=20):
         del m
     d32 = out["fp32"][0]
     res = {"workload": f"StereoUNet(base=32) eval forward, B=1, {W}x{H}, disparity+logvar (live app)",
-           "ms_fp8": round(ms["fp8"], 4), "ms_bf16": round(ms["bf16"], 4), "ms_fp32": round(ms["fp32"], 4),
+           "ms_fp8": round(ms["fp8"], 4), "ms_bf16": round(ms["bf16"], 4), "ms_bf16_fast": round(ms["bf16_fast"], 4),
+           "ms_fp32": round(ms["fp32"], 4),
+           "bf16_eval": "bf16: every weight as a hi/lo bf16 pair and BN-applied stores (the EPE-accurate eval forward, "
+                        "sd_conv3x3_ex); bf16_fast: BN-applied stores, plain bf16 weights",
            "pairs_per_s_fp8": round(1e3 / ms["fp8"], 2), "fwd_gflop": 255.87,
            "tflops_fp8": round(255.87e9 / (ms["fp8"] * 1e-3) / 1e12, 1),
            "mean_disparity_fp32": round(float(d32.mean()), 4),
@@ -310,7 +315,7 @@ def infer_fp8(torch, model, dev, H=720, W=960, iters=20):
                        "and heads bf16",
            "timing": f"mean of {iters} forwards after 3 (calibration, capture, replay): each precision's eval forward "
                      "replays a captured HIP graph"}
-    for prec in ("fp8", "bf16"):
+    for prec in ("fp8", "bf16", "bf16_fast"):
         res[f"epe_{prec}_vs_fp32"] = round(float((out[prec][0] - d32).abs().mean()), 5)
     return res
 

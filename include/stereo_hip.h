@@ -73,6 +73,11 @@ int sd_device_init(int device);
 /* ---- packing (weights are fp32 PyTorch layout in, dtype MFMA-ready layout out) ---- */
 /* reference input [B,6,H,W] f32 (train.py:320) -> NHWC dtype with cpad channels (zero pad). */
 int sd_pack_input(int dtype, const float* x_nchw, int batch, int cin, int H, int W, int cpad, void* out, sd_stream s);
+/* The same pack, also writing max |x| over the batch as float bits into amax[slot] (atomicMax into a zeroed word) and
+ * zeroing amax[clear] for a later call (clear < 0: none): the fp8 live loop's input-range check (a frame brighter than
+ * the calibration frame of the static e4m3 scales triggers a recalibration), read back asynchronously. */
+int sd_pack_input_amax(int dtype, const float* x_nchw, int batch, int cin, int H, int W, int cpad, void* out,
+                       unsigned* amax, int slot, int clear, sd_stream s);
 /* Conv2d(k3,p1,no bias) weight [co][ci][3][3] (model.py:36,39) -> fwd [co][kpad] (k = tap*ci_pad + ci)
  * or, dgrad != 0, the flipped/transposed [ci][kpad] (k = tap*co + o, W[o][ci][8-tap]). */
 int sd_pack_conv3_w(int dtype, const float* w, int co, int ci, int ci_pad, int dgrad, int kpad, void* out, sd_stream s);

@@ -111,6 +111,7 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_last_error": (ctypes.c_char_p, []),
     "sd_device_init": (_i, [_i]),
     "sd_pack_input": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _p]),
+    "sd_pack_input_amax": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p]),
     "sd_pack_conv3_w": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _p]),
     "sd_pack_convT_w": (_i, [_i, _p, _i, _i, _i, _i, _p, _p]),
     "sd_pack_weights": (_i, [_i, _PJOB, _i, _p, _p]),

@@ -51,6 +51,40 @@ __global__ void k_pack_input(const float* __restrict__ x, int batch, int cin, in
     }
 }
 
+// k_pack_input that also takes max |x| over the batch (the fp8 path's input-range check, engine._fp8_policy): per-block
+// reduce, one atomicMax of the float bits (|x| >= 0 orders like its bits) into amax[slot]; block 0 clears amax[clear]
+// for a later frame (the caller orders this kernel after the host's read-back of that slot)
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_input_amax(const float* __restrict__ x, int batch, int cin, int H, int W,
+                                                         int cpad, T* out, unsigned* amax, int slot, int clear) {
+    const long long P = (long long)batch * H * W;
+    const long long hw = (long long)H * W;
+    float m = 0.f;
+    for (long long px = blockIdx.x * 256LL + threadIdx.x; px < P; px += (long long)gridDim.x * 256) {
+        const long long b = px / hw, r = px - b * hw;
+        const float* src = x + b * cin * hw + r;
+        for (int c0 = 0; c0 < cpad; c0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                v[i] = c0 + i < cin ? src[(c0 + i) * hw] : 0.f;
+                m = fmaxf(m, fabsf(v[i]));
+            }
+            store8(out + px * cpad + c0, v);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    __shared__ float wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // skip the atomic unless this block raises the max (few blocks do: no contention)
+        const unsigned mb = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
+        if (mb > __hip_atomic_load(amax + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(amax + slot, mb);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 64 && clear >= 0) amax[clear] = 0u;
+}
+
 // fwd : out[o][tap*ci_pad + i] = w[o][i][tap]
 // dgrad: out[i][tap*co + o]    = w[o][i][8 - tap]
 template <typename T>
@@ -279,6 +313,22 @@ extern "C" int sd_pack_input(int dtype, const float* x, int batch, int cin, int 
         hipLaunchKernelGGL(k_pack_input<float>, dim3(g), dim3(256), 0, to_stream(s), x, batch, cin, H, W, cpad,
                            (float*)out);
     return sd_check_launch("sd_pack_input");
+}
+
+extern "C" int sd_pack_input_amax(int dtype, const float* x, int batch, int cin, int H, int W, int cpad, void* out,
+                                  unsigned* amax, int slot, int clear, sd_stream s) {
+    SD_REQUIRE(x && out && amax && batch > 0 && cin > 0 && H > 0 && W > 0 && slot >= 0 && clear != slot,
+               "sd_pack_input_amax: bad args");
+    SD_REQUIRE(cpad >= cin && cpad % 8 == 0, "sd_pack_input_amax: cpad %d", cpad);
+    int g = grid_for((long long)batch * H * W);
+    if (g > 512) g = 512;  // grid-stride: at most 512 block maxima compete for the atomic
+    if (dtype == SD_BF16)
+        hipLaunchKernelGGL(k_pack_input_amax<__bf16>, dim3(g), dim3(256), 0, to_stream(s), x, batch, cin, H, W, cpad,
+                           (__bf16*)out, amax, slot, clear);
+    else
+        hipLaunchKernelGGL(k_pack_input_amax<float>, dim3(g), dim3(256), 0, to_stream(s), x, batch, cin, H, W, cpad,
+                           (float*)out, amax, slot, clear);
+    return sd_check_launch("sd_pack_input_amax");
 }
 
 extern "C" int sd_pack_conv3_w(int dtype, const float* w, int co, int ci, int ci_pad, int dgrad, int kpad, void* out,

@@ -112,9 +112,15 @@ class UNetEngine:
         # fp8 recalibration triggers (_fp8_policy): input amax above margin x the calibration frame's, and age
         self.fp8_range_margin = float(os.environ.get("SD_FP8_RANGE_MARGIN", "1.25"))
         self.fp8_recalib_every = int(os.environ.get("SD_FP8_RECALIB_EVERY", "0"))
-        self.fp8_calibrations = self.fp8_range_recalibrations = self._fp8_age = 0
-        self._fp8_flag: torch.Tensor | None = None
-        self._fp8_flag_ev = None
+        self.fp8_calibrations = self.fp8_range_recalibrations = self._fp8_age = self._fp8_frame = 0
+        self._amax_dev: torch.Tensor | None = None  # [3] max |x| of the last frames' inputs (float bits), a ring
+        self._amax_host: torch.Tensor | None = None  # pinned copies
+        self._amax_ev: list = [None, None, None]
+        self._amax_used: list = [False, False, False]
+        self._amax_packed = None
+        self._amax_pending: int | None = None
+        self._fp8_cal = None  # (slot, event) of the calibration frame's amax
+        self._fp8_cal_amax: float | None = None
         # eval forwards of an unchanged state replay a captured HIP graph (SD_EVAL_GRAPH=0: eager launches)
         self.eval_graphs = os.environ.get("SD_EVAL_GRAPH", "1") != "0"
         self.sd_dtype = L.SD_F32 if precision == "fp32" else L.SD_BF16
@@ -169,8 +175,9 @@ class UNetEngine:
         self._one = torch.ones(16 * base_channels, dtype=torch.float32, device=self.device)
         self._zero = torch.zeros(16 * base_channels, dtype=torch.float32, device=self.device)
         mode = os.environ.get("SD_WSPLIT", "all")
-        self.wsplit = precision in ("bf16", "fp8") and mode != "0"
+        self.wsplit = precision == "bf16" and mode != "0"  # fp8: e4m3 dominates its error (measured: no gain)
         self.wsplit_train = self.wsplit and os.environ.get("SD_WSPLIT_TRAIN", "0") == "1"
+        self.wsplit_eval = True  # per-instance switch (bench.py times the bf16 eval forward both ways)
         offs = 0
         if self.wsplit:
             for cl in self.convs.values():
@@ -244,6 +251,10 @@ class UNetEngine:
         self.params, self.bufs = params, bufs
         self.grads = grads or {}
         self._watch = watch if watch is not None else list(params.values()) + list(bufs.values())
+        # fixed per bind: whether any watched tensor is an inference tensor (no version counter), and the storages
+        # (a rebind means new storages; _state_key then only reads the version counters: ~15 us instead of ~70)
+        self._watch_inference = any(t.is_inference() for t in self._watch)
+        self._bind_id = getattr(self, "_bind_id", 0) + 1
 
     def _s(self):
         return L.stream_handle(self.device)
@@ -254,9 +265,9 @@ class UNetEngine:
 
     def _state_key(self):
         """None when the state cannot be tracked (inference tensors carry no version counter)."""
-        if any(t.is_inference() for t in self._watch):
+        if self._watch_inference:
             return None
-        return (self.state_epoch, tuple((t.data_ptr(), t._version) for t in self._watch))
+        return (self.state_epoch, self._bind_id, tuple([t._version for t in self._watch]))
 
     def pack_weights(self, cached: bool = False):
         """Pack the weights into the kernels' layouts. cached=True (eval-mode inference): skip when the
@@ -324,7 +335,7 @@ class UNetEngine:
         return self.wsplit_pack.data_ptr() + 2 * off
 
     def _use_wsplit(self, layer, train: bool) -> bool:
-        return layer.off_s >= 0 and (not train or self.wsplit_train)
+        return layer.off_s >= 0 and self.wsplit_eval and (not train or self.wsplit_train)
 
     def _wp(self, off: int) -> int:
         return self.wpack.data_ptr() + off * self.wpack.element_size()
@@ -669,9 +680,11 @@ class UNetEngine:
             ws.coeff_key = key
         self.phase = "fwd"  # read by measurement hooks (bench.py) to tell forward from backward launches
         x = x.contiguous().float()
-        L.call("sd_pack_input", self.sd_dtype, x.data_ptr(), B, C, H, W, self.cin_pad0, ws.t["xin"].data_ptr(), self._s())
-        if self.fp8:
-            self._fp8_policy(ws)
+        if self.fp8 and self.fp8_static and self._q8_shapes:
+            self._pack_input_fp8(ws, x)
+        else:
+            L.call("sd_pack_input", self.sd_dtype, x.data_ptr(), B, C, H, W, self.cin_pad0, ws.t["xin"].data_ptr(),
+                   self._s())
         # eval forwards of an unchanged model state (the live app's loop): the launches after the input pack are
         # captured into a HIP graph on the second such forward and replayed from the third on (one host call instead
         # of 27-45 ctypes launches; B=1 960x720 forwards were host-bound at ~20 us of GPU time per kernel)
@@ -681,8 +694,10 @@ class UNetEngine:
             if ws.graph is not None and ws.graph_key == gkey:
                 with torch.cuda.device(self.device):  # replays on the current stream of the engine's device
                     ws.graph.replay()
+                self._amax_readback()
                 return ws
         self._forward_body(ws, train)
+        self._amax_readback()
         if gkey is not None and gkey[1] == self._fwd_path(ws):
             self._capture(ws, gkey, train)
         return ws
@@ -693,45 +708,74 @@ class UNetEngine:
         if self.ws is not None:
             self.ws.q8_ready = False
 
-    def _fp8_policy(self, ws: Workspace):
+    def _fp8_policy(self, ws: Workspace, slot: int):
         """Static fp8 scales come from one calibration frame; a later frame with a wider range would saturate at
-        +-448. Two triggers make the next forward a calibration forward again:
-          * range: every static forward compares its packed input's amax with the calibration frame's (one small
-            reduction, the flag copied to pinned host memory without a sync); a frame above `fp8_range_margin` x the
-            calibrated amax triggers recalibration at the following forward (one frame late, no host stall);
+        +-448. Two triggers make this forward a calibration forward again:
+          * range: the input pack of every static forward also takes max |x| (sd_pack_input_amax, no extra pass),
+            read back to pinned memory without a sync; when a frame's amax exceeds `fp8_range_margin` x the calibration
+            frame's, the next forward recalibrates (one frame late, no host stall);
           * age: every `fp8_recalib_every` static forwards (0: never).
-        `fp8_calibrations` counts calibration forwards."""
-        if not (self.fp8_static and self._q8_shapes):
-            return
-        if not ws.q8_ready or self._eval_coeffs:  # this forward calibrates (new state, new workspace, or requested)
+        `fp8_calibrations` counts calibration forwards. Returns whether this forward calibrates."""
+        if not ws.q8_ready or self._eval_coeffs:  # new state, new workspace, or requested
+            return True
+        if self._fp8_cal_amax is None and self._fp8_cal is not None:  # the calibration frame's amax, once it landed
+            s, ev = self._fp8_cal
+            ev.synchronize()  # recorded a frame ago: normally complete already
+            self._fp8_cal_amax = float(self._amax_host[s])
+        prev = (slot + 2) % 3
+        ev = self._amax_ev[prev]
+        if (self.fp8_range_margin > 0 and self._amax_used[prev] and ev.query() and self._fp8_cal_amax is not None
+                and float(self._amax_host[prev]) > self.fp8_range_margin * self._fp8_cal_amax):
+            self.fp8_range_recalibrations += 1
+            return True
+        if self.fp8_recalib_every and self._fp8_age >= self.fp8_recalib_every:
+            return True
+        self._fp8_age += 1
+        return False
+
+    def _pack_input_fp8(self, ws: Workspace, x: torch.Tensor):
+        """The static-scale fp8 path's input pack: sd_pack_input + the input amax for _fp8_policy. A ring of three
+        device words: frame f takes word f % 3 and zeroes word (f + 1) % 3, after the launch stream has waited for the
+        side-stream read-back of that word (frame f - 2's, long complete: a barrier packet, no stall)."""
+        B, C, H, W = x.shape
+        slot = self._fp8_frame % 3
+        clear = (slot + 1) % 3
+        self._fp8_frame += 1
+        if self._amax_dev is None:
+            with torch.inference_mode(False):  # written in place by later forwards, in or out of inference mode
+                self._amax_dev = torch.zeros(3, dtype=torch.float32, device=self.device)
+                self._amax_host = torch.zeros(3, dtype=torch.float32, pin_memory=True)
+            self._amax_ev = [torch.cuda.Event() for _ in range(3)]
+            self._amax_used = [False] * 3
+            self._amax_packed = torch.cuda.Event()
+        if self._fp8_policy(ws, slot):
+            ws.q8_ready = False
             self.fp8_calibrations += 1
             self._fp8_age = 0
-            ws.t.pop("cal_amax", None)
-            self._fp8_flag_ev = None
-            return
-        ev = self._fp8_flag_ev
-        if ev is not None and ev.query() and int(self._fp8_flag[0]) != 0:
-            self._fp8_flag[0] = 0
-            self._fp8_flag_ev = None
-            self.fp8_range_recalibrations += 1
-            ws.q8_ready = False
-        elif self.fp8_recalib_every and self._fp8_age >= self.fp8_recalib_every:
-            ws.q8_ready = False
+            self._fp8_cal_amax = None
+        main = torch.cuda.current_stream(self.device)
+        if self._amax_used[clear]:
+            main.wait_event(self._amax_ev[clear])
+        L.call("sd_pack_input_amax", self.sd_dtype, x.data_ptr(), B, C, H, W, self.cin_pad0, ws.t["xin"].data_ptr(),
+               self._amax_dev.data_ptr(), slot, clear, self._s())
+        self._amax_packed.record(main)
+        self._amax_pending = slot  # read back by _amax_readback once the forward's launches are queued
         if not ws.q8_ready:
-            return self._fp8_policy(ws)
-        self._fp8_age += 1
-        if self.fp8_range_margin > 0:
-            t = ws.t
-            inf = float("inf")
-            if "cal_amax" not in t:  # mm:xin still holds the calibration frame's per-channel (min, max) rows
-                t["cal_amax"] = torch.linalg.vector_norm(t["mm:xin"], ord=inf)
-            cur = torch.linalg.vector_norm(t["xin"], ord=inf).float()  # a max: exact in bf16
-            flag = (cur > self.fp8_range_margin * t["cal_amax"]).to(torch.int32)
-            if self._fp8_flag is None:
-                self._fp8_flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self._fp8_flag.copy_(flag.view(1), non_blocking=True)
-            self._fp8_flag_ev = torch.cuda.Event()
-            self._fp8_flag_ev.record(torch.cuda.current_stream(self.device))
+            self._fp8_cal = (slot, self._amax_ev[slot])
+
+    def _amax_readback(self):
+        """The input amax of this frame -> pinned host memory on a side stream, queued after the forward's launches
+        (the 4-byte copy on the launch stream, and its host calls before the graph replay, cost ~25 us per frame)."""
+        slot = self._amax_pending
+        if slot is None:
+            return
+        self._amax_pending = None
+        side = self._side_stream()
+        side.wait_event(self._amax_packed)
+        with torch.cuda.stream(side):
+            self._amax_host[slot:slot + 1].copy_(self._amax_dev[slot:slot + 1], non_blocking=True)
+            self._amax_ev[slot].record(side)
+        self._amax_used[slot] = True
 
     def _capture(self, ws: Workspace, gkey, train: bool):
         """Capture the forward body into a HIP graph on the engine's OWN capture stream on its device (torch's shared

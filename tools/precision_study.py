@@ -192,6 +192,10 @@ def main():
         cfgs = {"bf16": {}, "wsplit enc1.0": {"wsplit": ["enc1.0"]},
                 "wsplit full-res": {"wsplit": ["enc1.0", "enc1.1", "dec1.0", "dec1.1", "up1"]},
                 "wsplit all": {"wsplit": LAYERS}}
+        if "--product" in sys.argv:  # the engine's eval forward options
+            cfgs = {"wsplit all + zstore": {"wsplit": LAYERS, "zstore": CONVS},
+                    "wsplit convs + zstore": {"wsplit": CONVS, "zstore": CONVS},
+                    "zstore only": {"zstore": CONVS}}
         if "--actgroups" in sys.argv:  # with every weight split: which activation roundings carry the noise
             dec = [l for l in LAYERS if l.startswith(("dec", "up"))]
             enc = [l for l in LAYERS if l.startswith(("enc", "bott"))]
