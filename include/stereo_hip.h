@@ -144,6 +144,15 @@ int sd_conv3x3_ex(const sd_src* a, int batch, int H, int W, const void* wpack, i
                   const float* out_scale, const float* out_shift, void* out, float* stats, sd_stream s);
 int sd_conv3x3_ex_ok(const sd_src* a, int N);
 const char* sd_conv3x3_ex_kernel_name(const sd_src* a, int H, int W, int N, int epi, int flags, int out_affine);
+/* The same with a split-K workspace: a STORE launch whose items would leave most CUs idle (the batch-1 forwards of the
+ * deep layers) runs in groups of blocks over slices of the input-channel chunks (and of the hi/lo passes), and a
+ * second launch adds their fp32 partial sums, applies the output affine and stores bf16. ws (16-B aligned) must hold
+ * sd_conv3x3_ex_ws_bytes(...) bytes (0: no split for the shape); a NULL or smaller ws runs unsplit. Results equal
+ * sd_conv3x3_ex's up to the fp32 summation order. */
+long long sd_conv3x3_ex_ws_bytes(const sd_src* a, int batch, int H, int W, int N, int epi, int flags);
+int sd_conv3x3_ex_ws(const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, int flags,
+                     const float* out_scale, const float* out_shift, void* out, float* stats, void* ws,
+                     long long ws_bytes, sd_stream s);
 int sd_conv_gemm_bnsum_rows(const sd_src* a, int batch, int H, int W, int N);
 const char* sd_conv_gemm_bnsum_kernel_name(const sd_src* a, int H, int W, int N);
 
@@ -311,7 +320,14 @@ int sd_fp8_qparams(const sd_qsrc* src, int nsrc, float* act_scale, sd_stream s);
  * channels; a concatenation's first source a multiple of 16 channels). */
 int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
                   const float* act_scale, int N, int kpad, void* out, sd_stream s);
-const char* sd_conv3x3_q8_kernel_name(int H, int W, int N, int c0, int c1);
+/* The same with a split-K workspace: where the layer's items would leave most CUs idle (the batch-1 forwards of the
+ * deep layers) groups of blocks take slices of the input channels and a second launch adds their fp32 partial sums.
+ * ws (16-B aligned) must hold sd_conv3x3_q8_ws_bytes(batch, H, W, N, c0, c1) bytes (0: no split for the shape); a
+ * NULL or smaller ws runs the unsplit kernel. Results equal sd_conv3x3_q8's up to fp32 summation order. */
+long long sd_conv3x3_q8_ws_bytes(int batch, int H, int W, int N, int c0, int c1);
+int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
+                     const float* act_scale, int N, int kpad, void* out, void* ws, long long ws_bytes, sd_stream s);
+const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1);
 
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----
  * One flat fp32 parameter/gradient/state buffer (all tensors share lr/betas/eps/wd).

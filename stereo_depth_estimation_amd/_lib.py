@@ -123,6 +123,8 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_conv_gemm_bnsum_kernel_name": (ctypes.c_char_p, [_SRC, _i, _i, _i]),
     "sd_conv_gemm_kernel_name": (ctypes.c_char_p, [_i, _SRC, _i, _i, _i, _i, _i]),
     "sd_conv3x3_ex": (_i, [_SRC, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "sd_conv3x3_ex_ws": (_i, [_SRC, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, ctypes.c_longlong, _p]),
+    "sd_conv3x3_ex_ws_bytes": (ctypes.c_longlong, [_SRC, _i, _i, _i, _i, _i, _i]),
     "sd_conv3x3_ex_ok": (_i, [_SRC, _i]),
     "sd_conv3x3_ex_kernel_name": (ctypes.c_char_p, [_SRC, _i, _i, _i, _i, _i, _i]),
     "sd_wgrad_kernel_name": (ctypes.c_char_p, [_i, _SRC, _SRC, _i, _i]),
@@ -159,7 +161,9 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_pack_conv3_w_fp8": (_i, [_p, _i, _i, _i, _i, _p, _p, _p]),
     "sd_conv3x3_fp8": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p, _p]),
     "sd_conv3x3_q8": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p]),
-    "sd_conv3x3_q8_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
+    "sd_conv3x3_q8_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
+    "sd_conv3x3_q8_ws_bytes": (ctypes.c_longlong, [_i, _i, _i, _i, _i, _i]),
+    "sd_conv3x3_q8_ws": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p, ctypes.c_longlong, _p]),
     "sd_conv3x3_fp8_rows": (_i, [_i, _i, _i, _i]),
     "sd_conv3x3_fp8_kernel_name": (ctypes.c_char_p, [_i]),
     "sd_chan_minmax_rows": (_i, [_i64, _i]),
@@ -214,7 +218,7 @@ def kernel_name(name: str, *args) -> str:
 def call(name: str, *args) -> int:
     """Call an int-returning entry point; raise StereoHipError with sd_last_error() on failure."""
     lib = load()
-    if name.endswith(("_rows", "_splits", "_ok")) or name == "sd_version":
+    if name.endswith(("_rows", "_splits", "_ok", "_bytes")) or name == "sd_version":
         return getattr(lib, name)(*args)
     if _hook is not None:
         _hook(name, args, "pre")

@@ -279,7 +279,9 @@ const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool 
                              bool oaff = false);
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns = nullptr,
-                     bool wsplit = false, const float* osc = nullptr, const float* osh = nullptr);
+                     bool wsplit = false, const float* osc = nullptr, const float* osh = nullptr, void* ws = nullptr,
+                     long long ws_bytes = 0);
+long long sd_halo_split_ws_bytes(const sd_src& a, int batch, int H, int W, int N, int epi, bool wsplit);
 int sd_halo_store_rows(int batch, int H, int W, int N, int ctot);
 bool sd_halo_bnsum_ok(const sd_src& a, int N);
 
@@ -419,9 +421,14 @@ extern "C" const char* sd_conv3x3_ex_kernel_name(const sd_src* a, int H, int W, 
     return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1], false, (flags & SD_CONV_WSPLIT) != 0, oaff != 0);
 }
 
-extern "C" int sd_conv3x3_ex(const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi,
-                             int flags, const float* out_scale, const float* out_shift, void* out, float* stats,
-                             sd_stream s) {
+extern "C" long long sd_conv3x3_ex_ws_bytes(const sd_src* a, int batch, int H, int W, int N, int epi, int flags) {
+    if (!a || !sd_conv3x3_ex_ok(a, N) || batch <= 0) return 0;
+    return sd_halo_split_ws_bytes(*a, batch, H, W, N, epi, (flags & SD_CONV_WSPLIT) != 0);
+}
+
+extern "C" int sd_conv3x3_ex_ws(const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi,
+                                int flags, const float* out_scale, const float* out_shift, void* out, float* stats,
+                                void* ws, long long ws_bytes, sd_stream s) {
     if (int e = validate_src(a, "sd_conv3x3_ex")) return e;
     SD_REQUIRE(sd_conv3x3_ex_ok(a, N), "sd_conv3x3_ex: bf16 3x3 halo shapes only (N = 32 or N %% 64 == 0)");
     SD_REQUIRE(epi == SD_EPI_STORE || epi == SD_EPI_STATS, "sd_conv3x3_ex: epi %d (STORE or STATS)", epi);
@@ -432,9 +439,16 @@ extern "C" int sd_conv3x3_ex(const sd_src* a, int batch, int H, int W, const voi
                "sd_conv3x3_ex: bad args");
     GatherSrc g = make_gather(*a);
     SD_REQUIRE(g.Hl == H && g.Wl == W, "sd_conv3x3_ex: source grid %dx%d != GEMM grid %dx%d", g.Hl, g.Wl, H, W);
-    const bool ws = (flags & SD_CONV_WSPLIT) != 0;
-    SD_REQUIRE(kpad % 64 == 0 && kpad >= (ws ? 2 : 1) * g.kchunks * 8, "sd_conv3x3_ex: kpad %d < K (%d)", kpad,
-               (ws ? 2 : 1) * g.kchunks * 8);
-    return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, epi, out, nullptr, 0, stats, to_stream(s), nullptr, ws,
-                            out_scale, out_shift);
+    const bool wsp = (flags & SD_CONV_WSPLIT) != 0;
+    SD_REQUIRE(kpad % 64 == 0 && kpad >= (wsp ? 2 : 1) * g.kchunks * 8, "sd_conv3x3_ex: kpad %d < K (%d)", kpad,
+               (wsp ? 2 : 1) * g.kchunks * 8);
+    return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, epi, out, nullptr, 0, stats, to_stream(s), nullptr, wsp,
+                            out_scale, out_shift, ws, ws_bytes);
+}
+
+extern "C" int sd_conv3x3_ex(const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi,
+                             int flags, const float* out_scale, const float* out_shift, void* out, float* stats,
+                             sd_stream s) {
+    return sd_conv3x3_ex_ws(a, batch, H, W, wpack, N, kpad, epi, flags, out_scale, out_shift, out, stats, nullptr, 0,
+                            s);
 }

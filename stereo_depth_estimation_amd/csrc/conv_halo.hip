@@ -218,6 +218,13 @@ struct HFwdArgs {
     // xhat = (by-mean)*invstd (what sd_bn_bwd_reduce computes in a pass of its own)
     const __bf16* by;
     const float *bsc, *bsh, *bmu, *bis;
+    // split-K (eval STORE launches whose items leave most CUs idle: the batch-1 forwards of the deep layers): ksplit
+    // groups of gblk = gper * nblk blocks, group ks runs chunks [ks*cps, ks*cps + cps) of every item (wsplit: of the
+    // 2 x ncp hi/lo chunks) and stores its raw fp32 sums to part[ks][pixel][N]; k_halo_split_reduce adds the groups'
+    // partials, applies the output affine (OAFF) and stores bf16. ksplit = 1: part is null, the epilogue stores out0.
+    int ksplit, gblk, cps;
+    int npix;  // batch * H * W (partials rows per group)
+    float* part;
 };
 
 // Cache policy of the conv epilogue stores: nontemporal (2). The outputs (0.1-0.3 GB per launch) are read by the next
@@ -343,7 +350,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // Renumbered so that each XCD owns a contiguous range of block ids, the tiles a wave of items covers
     // on one XCD are neighbours (shared halo rows, and the N-blocks of one tile) and meet in that L2.
     const int bid = p.xcd ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-    const int nb = bid % p.nblk, slot = bid / p.nblk;
+    const int ks = bid / p.gblk, bb = bid - ks * p.gblk;  // split-K group, block within the group
+    const int nb = bb % p.nblk, slot = bb / p.nblk;
     const int n0 = nb * BN;
     // chunks never straddle the two sources (a source's last chunk may be partial): every chunk has one
     // source, one channel stride and one BN affine
@@ -353,7 +361,9 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // to ~2^-17 relative), so the sum over both passes is the product with the fp32 weights: the full-resolution
     // layers' weight rounding is what moved the bf16 path's EPE (tools/precision_study.py). The MFMA waves see
     // 2 x ncp chunks per item; only the loaders know which pass a chunk belongs to.
-    const int nchunks = p.wsplit ? 2 * ncp : ncp;
+    const int nch_v = p.wsplit ? 2 * ncp : ncp;
+    const int c_lo = ks * p.cps;  // split-K: this group's chunks [c_lo, c_lo + nchunks)
+    const int nchunks = (c_lo + p.cps < nch_v ? c_lo + p.cps : nch_v) - c_lo;
     const int wct = p.wsplit ? 2 * p.a.ctot : p.a.ctot;  // packed weight channels per tap
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
@@ -368,20 +378,24 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // the BN affine of every input channel (identity for raw sources), read by the loaders per chunk from LDS
     __shared__ __attribute__((aligned(16))) float sbn[2 * SBN_MAX + 2 * CK];  // + the tail of a partial chunk
     __shared__ __attribute__((aligned(16))) float oaff[OAFF ? 2 * BN : 4];      // OAFF: [scale | shift] of this N-block
-    if constexpr (OAFF) {
-        for (int c = tid; c < 2 * BN; c += 512) {
-            const int ch = n0 + (c < BN ? c : c - BN);
-            oaff[c] = ch < p.N ? (c < BN ? p.osc : p.osh)[ch] : 0.f;
+    // The tables are filled by both roles, each before the launch's first barrier; the loaders issue their first
+    // chunks' loads before their share (VMEM loads complete in order, so one memory latency covers the tables, the
+    // weights and the first halos instead of one each: the serial latencies are what a batch-1 launch costs)
+    auto fill_tables = [&]() __attribute__((always_inline)) {
+        if constexpr (OAFF) {
+            for (int c = tid; c < 2 * BN; c += 512) {
+                const int ch = n0 + (c < BN ? c : c - BN);
+                oaff[c] = ch < p.N ? (c < BN ? p.osc : p.osh)[ch] : 0.f;
+            }
         }
-    }
-    for (int c = tid; c < p.a.ctot; c += 512) {
-        const bool first = c < p.a.c0;
-        const int cl = first ? c : c - p.a.c0;
-        const bool bn = (first ? p.a.x0 : p.a.x1) == SD_BNRELU;
-        sbn[c] = bn ? (first ? p.a.sc0 : p.a.sc1)[cl] : 1.f;
-        sbn[SBN_MAX + c] = bn ? (first ? p.a.sh0 : p.a.sh1)[cl] : 0.f;
-    }
-    __syncthreads();
+        for (int c = tid; c < p.a.ctot; c += 512) {
+            const bool first = c < p.a.c0;
+            const int cl = first ? c : c - p.a.c0;
+            const bool bn = (first ? p.a.x0 : p.a.x1) == SD_BNRELU;
+            sbn[c] = bn ? (first ? p.a.sc0 : p.a.sc1)[cl] : 1.f;
+            sbn[SBN_MAX + c] = bn ? (first ? p.a.sh0 : p.a.sh1)[cl] : 0.f;
+        }
+    };
     float* const redf = sbn;  // [4][BN][2] BN statistics after the last item (the loaders no longer read sbn)
     static_assert(4 * BN * 2 <= 2 * SBN_MAX, "redf fits in sbn");
 
@@ -477,9 +491,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         // they are loaded once and stored into the two buffers in the prologue (one chunk: into both). Two-chunk
         // layers (64 input channels: enc2.1, dec2.1, enc3.0, dec1.0, ...) re-staged 36-72 KB of weights per item
         int w_cc = 0;  // chunk (within the item) of the next weights to load
-        auto load_w = [&]() __attribute__((always_inline)) {  // weights of chunk w_cc -> wr, then advance
-            const bool lo = w_cc >= ncp;  // wsplit: the second pass reads the lo halves
-            const int wc = lo ? w_cc - ncp : w_cc;
+        auto load_w_into = [&](uint4 (&wdst)[W_PER_THREAD]) __attribute__((always_inline)) {  // chunk w_cc, advance
+            const int wv = c_lo + w_cc;
+            const bool lo = wv >= ncp;  // wsplit: the second pass reads the lo halves
+            const int wc = lo ? wv - ncp : wv;
             const bool s1 = wc >= nc0;
             const int C = s1 ? p.a.c1 : p.a.c0;
             const int cl = (s1 ? wc - nc0 : wc) * CK;
@@ -499,22 +514,25 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
 #pragma unroll
             for (int i = 0; i < W_PER_THREAD; ++i) {
                 const auto x = __builtin_amdgcn_raw_buffer_load_b128(wrs, v[i], cbg * 2, 0);
-                wr[i] = make_uint4(x[0], x[1], x[2], x[3]);
+                wdst[i] = make_uint4(x[0], x[1], x[2], x[3]);
             }
         };
-        auto store_w = [&](int buf) __attribute__((always_inline)) {
+        auto load_w = [&]() __attribute__((always_inline)) { load_w_into(wr); };
+        auto store_w_from = [&](int buf, const uint4 (&wsrc)[W_PER_THREAD]) __attribute__((always_inline)) {
             __bf16* wl = smem + buf * BUF + HALO_ELEMS;
 #pragma unroll
             for (int i = 0; i < W_PER_THREAD; ++i) {
                 const int item = ltid + i * 256;
                 const int co = item / (9 * PPX), r = item - co * (9 * PPX);
                 const int rs = M16 ? r ^ wswz(co) : r;  // M16: pieces swapped by row (conflict-free 16x16 reads)
-                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * W_LD + rs * 8) = wr[i];
+                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * W_LD + rs * 8) = wsrc[i];
             }
         };
+        auto store_w = [&](int buf) __attribute__((always_inline)) { store_w_from(buf, wr); };
         auto load = [&](auto S) __attribute__((always_inline)) {  // halo of chunk (ld_item, ld_cc) -> register set S, then advance
             HSet& q = set_of(S);
-            const int hc = ld_cc >= ncp ? ld_cc - ncp : ld_cc;  // wsplit: the second pass re-reads the same halo
+            const int hv = c_lo + ld_cc;
+            const int hc = hv >= ncp ? hv - ncp : hv;  // wsplit: the second pass re-reads the same halo
             const bool s1 = hc >= nc0;
             const int C = s1 ? p.a.c1 : p.a.c0;
             const int cl = (s1 ? hc - nc0 : hc) * CK;
@@ -605,16 +623,18 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             __syncthreads();
             stamp(t_br);
         };
+        // WCONST: the second chunk's weights (two chunks per item) in registers of their own, so both loads are in
+        // flight with the first halos
+        uint4 wr2[WCONST ? W_PER_THREAD : 1];
         if (total > 0) {
             // the loads an iteration would have issued before chunk 0: the halo of chunks 0 .. LS-2, the weights
-            // of chunk 0, the halo of chunk LS-1 (WCONST: the weights first, stored right away)
+            // of chunk 0, the halo of chunk LS-1 (WCONST: the weights of both chunks first, stored after the tables)
             // sched barriers: the issue order must be an iteration's (the scheduler may swap independent sets)
             geometry();
             if constexpr (WCONST) {
                 load_w();  // chunk 0
-                store_w(0);
-                load_w();  // chunk 1 (chunk 0 again with one chunk per item)
-                store_w(1);
+                if (nchunks > 1) load_w_into(wr2);  // chunk 1
+                __builtin_amdgcn_sched_barrier(0);
             }
             load(S0);
             __builtin_amdgcn_sched_barrier(0);
@@ -628,6 +648,15 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (LS == 4) load(S3);
             else load(S1);
+        }
+        fill_tables();
+        __syncthreads();  // the tables (the MFMA waves meet it before their first chunk)
+        if (total > 0) {
+            if constexpr (WCONST) {
+                store_w(0);
+                if (nchunks > 1) store_w_from(1, wr2);
+                else store_w(1);  // one chunk per item: chunk 0 in both buffers
+            }
             // a multiple of LS iterations, no exit between them (an exit between the sets made the compiler's
             // vmcnt bookkeeping drain every load in half of them); the iterations past the last chunk store
             // zeros into buffers the MFMA waves no longer read, and they meet them with extra barriers
@@ -652,12 +681,25 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     }
 
     // =============================================================== MFMA waves
+    fill_tables();
+    __syncthreads();  // the tables
+    // 32-pixel column tile i of this MFMA wave: the M16 instances own RT consecutive ones (in 32-pixel-wide tiles, RT
+    // consecutive rows: what the vertical-reuse k-loop below needs), the others every fourth
+    auto tile_T = [&](int i) { return M16 ? wid * RT + i : wid + 4 * i; };
+    // Vertical reuse (the N = 32 RT = 4 instances: full-resolution 16x32 tiles, 4 rows per wave): the taps of one kernel
+    // column kw meet the same halo fragments one row apart, so each 16-pixel halo fragment (row hr, half h, shifted by
+    // kw) is read once and feeds the up-to-3 output rows hr - kh: (RT + 2) x 2 reads per kw instead of 3 x 2RT, 40 %
+    // fewer of the LDS fragment reads that paced the full-resolution layers' MFMA phase. HC_VR=0 builds: the per-tap loop.
+#ifndef HC_VR
+#define HC_VR 1
+#endif
+    constexpr bool VR = HC_VR && M16 && NT == 1 && RT == 4;
     // B-fragment (pixel) halo offsets of this lane's columns (tap (0,0)), the same for every tile;
     // columns past the tile read pixel 0 and are masked in the epilogue
     int abase[RT];
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-        const int m = (wid + 4 * i) * 32 + (lane & 31);
+        const int m = tile_T(i) * 32 + (lane & 31);
         const int hm = m / p.tw, wm = m - hm * p.tw;
         abase[i] = m < mvalid ? hm * p.hw + wm : 0;
     }
@@ -666,7 +708,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     if constexpr (M16) {
 #pragma unroll
         for (int i = 0; i < 2 * RT; ++i) {
-            const int m = (wid + 4 * (i >> 1)) * 32 + (i & 1) * 16 + (lane & 15);
+            const int m = tile_T(i >> 1) * 32 + (i & 1) * 16 + (lane & 15);
             const int hm = m / p.tw, wm = m - hm * p.tw;
             abase16[i] = (lane >> 4) * HPX * 8 + (m < mvalid ? hm * p.hw + wm : 0) * 8;
         }
@@ -701,7 +743,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int r = 0; r < ER; ++r) {
-            const int m = (wid + 4 * i) * 32 + r * EPR + lane / PPP;
+            const int m = tile_T(i) * 32 + r * EPR + lane / PPP;
             const int hm = m / p.tw, wm = m - hm * p.tw;
             const unsigned v = m < mvalid ? (unsigned)((hm << 9) | wm) : 0xffffu;
             const int k = i * ER + r;
@@ -714,7 +756,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     int eoff[NEO];
 #pragma unroll
     for (int k = 0; k < NEO; ++k) {
-        const int m = (wid + 4 * (k / ER)) * 32 + (k % ER) * EPR + lane / PPP;
+        const int m = tile_T(k / ER) * 32 + (k % ER) * EPR + lane / PPP;
         const int hm = m / p.tw, wm = m - hm * p.tw;
         eoff[k] = m < mvalid ? hm * p.W + wm : -1;
     }
@@ -830,8 +872,58 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             for (int i = 0; i < RT; ++i)
                 af[slot_][u][i] = *reinterpret_cast<const bf16x8*>(hx + u * HALO_ITEM + (abase[i] + toff) * HX_LD + c8 * 8);
         };
-        if constexpr (M16) {
+        if constexpr (VR) {
           if (!(WG_EXP & 8)) {
+            constexpr int R = RT, NH = R + 2, NS = 3 * NH, PV = 2;  // rows, halo rows, steps (kw, hr), read-ahead
+            constexpr int HWV = 34;                                 // halo width of a 32-pixel-wide tile
+            // weights of taps (kh, kw), 16-channel blocks t: one set; column kw+1's kh = 0, 1 are read during column
+            // kw's last row step (which uses kh = 2 only), its kh = 2 during column kw+1's first (kh = 0 only)
+            bf16x8 av[3][2];
+            bf16x8 xv[PV + 1][2];    // halo fragments of step s (halves h), ring
+            const __bf16* const xb = hx + (lane >> 4) * HPX * 8 + (wid * RT * HWV + (lane & 15)) * 8;
+            auto readA = [&](int kw, int kh) __attribute__((always_inline)) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                    av[kh][t] = *reinterpret_cast<const bf16x8*>(
+                        wl + (t * 16 + (lane & 15)) * W_LD + (kh * 3 + kw) * CK + ((lane >> 4) ^ wswz(lane & 15)) * 8);
+            };
+            auto readX = [&](int st) __attribute__((always_inline)) {
+                const int kw = st / NH, hr = st % NH;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    xv[st % (PV + 1)][h] = *reinterpret_cast<const bf16x8*>(xb + (hr * HWV + h * 16 + kw) * 8);
+            };
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) readA(0, kh);
+#pragma unroll
+            for (int st = 0; st < PV; ++st) readX(st);
+#pragma unroll
+            for (int st = 0; st < NS; ++st) {
+                const int kw = st / NH, hr = st % NH;
+                if (hr == NH - 1 && kw < 2) {  // this step uses kh = 2 only
+                    readA(kw + 1, 0);
+                    readA(kw + 1, 1);
+                }
+                if (hr == 0 && kw > 0) readA(kw, 2);  // this step uses kh = 0 only
+                if (st + PV < NS) readX(st + PV);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    const int r = hr - kh;  // output row of this (halo row, kernel row) pair
+                    if (r < 0 || r >= R) continue;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+                            acc4[2 * r + h][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                av[kh][t], xv[st % (PV + 1)][h], acc4[2 * r + h][t], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+        if constexpr (M16) {
+          if (!VR && !(WG_EXP & 8)) {
             // one k-step per tap: A = 16 weight rows x 32 channels, B = 32 channels x 16 halo pixels
             bf16x8 a16[PF + 1][2 * NT], b16[PF + 1][2 * RT];
             auto read16 = [&](int tap) {
@@ -898,6 +990,38 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
             const int ty = tl / p.tiles_x;
             const int h0 = ty * p.th, w0 = (tl - ty * p.tiles_x) * p.tw;
             const int hw_img = p.H * p.W;
+            if constexpr (!STATS && !BNS) {
+                if (p.part) {
+                    // split-K partials straight from the accumulators (4 consecutive channels of one pixel per 16-B
+                    // store; batch-1 sizes, a few MB per launch)
+                    float* const pk = p.part + ((size_t)ks * p.npix + (size_t)b * hw_img) * p.N;
+                    auto put = [&](int m, int c, float a0, float a1, float a2, float a3) __attribute__((always_inline)) {
+                        const int hm = m / p.tw, wm = m - hm * p.tw;
+                        if ((m < mvalid) & (h0 + hm < p.H) & (w0 + wm < p.W) & (n0 + c < p.N))
+                            *reinterpret_cast<float4*>(pk + ((size_t)(h0 + hm) * p.W + w0 + wm) * p.N + n0 + c) =
+                                make_float4(a0, a1, a2, a3);
+                    };
+                    if constexpr (M16) {
+#pragma unroll
+                        for (int i2 = 0; i2 < 2 * RT; ++i2)
+#pragma unroll
+                            for (int t = 0; t < 2 * NT; ++t)
+                                put(tile_T(i2 >> 1) * 32 + (i2 & 1) * 16 + (lane & 15), t * 16 + 4 * (lane >> 4),
+                                    acc4[i2][t][0], acc4[i2][t][1], acc4[i2][t][2], acc4[i2][t][3]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < RT; ++i)
+#pragma unroll
+                            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                                for (int g4 = 0; g4 < 4; ++g4)
+                                    put(tile_T(i) * 32 + (lane & 31), t * 32 + 8 * g4 + 4 * (lane >> 5),
+                                        acc[u][i][t][4 * g4], acc[u][i][t][4 * g4 + 1], acc[u][i][t][4 * g4 + 2],
+                                        acc[u][i][t][4 * g4 + 3]);
+                    }
+                    continue;
+                }
+            }
             const bool split = p.epi == SD_EPI_SPLIT || p.epi == SD_EPI_SPLIT_STATS;
             const int ns = split ? p.n_split : p.N;
             const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
@@ -1979,6 +2103,73 @@ const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool 
 
 // wconst (one or two chunks per item): the weights are staged once per block. CK = 8 always has one chunk; CK = 16
 // (experiments) always takes the general instance, which is also correct with one chunk.
+// sum of the split-K partials part[ks][pixel][N] (fp32, the groups in order: deterministic), then the output affine
+// (OAFF launches) -> bf16 out[pixel][N]; 8 channels per thread
+__global__ __launch_bounds__(256) void k_halo_split_reduce(const float* __restrict__ part, int ksplit, long long n8, int N,
+                                                           const float* __restrict__ osc, const float* __restrict__ osh,
+                                                           __bf16* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const float4* src = reinterpret_cast<const float4*>(part) + 2 * i;
+    float v[8];
+    {
+        const float4 a = src[0], b = src[1];
+        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    }
+    for (int k = 1; k < ksplit; ++k) {
+        const float4 a = src[(size_t)k * 2 * n8], b = src[(size_t)k * 2 * n8 + 1];
+        v[0] += a.x, v[1] += a.y, v[2] += a.z, v[3] += a.w, v[4] += b.x, v[5] += b.y, v[6] += b.z, v[7] += b.w;
+    }
+    if (osc) {
+        const int c = (int)((8 * i) % N);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], osc[c + j], osh[c + j]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
+    reinterpret_cast<bf16x8*>(out)[i] = o;
+}
+
+// split-K plan of an eval STORE launch (SD_HALO_SPLIT=0 disables it and the 32-channel N-blocks, for A/B runs): where
+// the grid has fewer than 128 blocks, 32-channel N-blocks for N % 64 == 0 (twice the blocks) and then groups of blocks
+// over slices of the chunks, up to 256 blocks with at least one chunk each
+struct HSplit {
+    int ksplit, cps, nblk, gper;
+    bool nt1;
+};
+static HSplit halo_split_plan(const HTile& t, int nblk, int gper, int nsp, int N, int nch_v, int epi, bool bns) {
+    static const bool on = [] {
+        const char* e = getenv("SD_HALO_SPLIT");
+        return !(e && atoi(e) == 0);
+    }();
+    HSplit q{1, nch_v, nblk, gper, false};
+    if (!on || epi != SD_EPI_STORE || bns || t.it != 1 || t.ck == 16) return q;
+    auto grid_of = [&](int nb) {
+        q.nblk = nb;
+        q.gper = PERSIST_BLOCKS / nb;
+        if (q.gper < 1) q.gper = 1;
+        if (q.gper > nsp) q.gper = nsp;
+        q.ksplit = 1;
+        q.cps = nch_v;
+        const int gblk = q.gper * nb;
+        if (gblk < 128 && nch_v >= 2) {
+            int ks = PERSIST_BLOCKS / gblk;
+            if (ks > nch_v) ks = nch_v;
+            if (ks > 1) {
+                q.cps = cdiv(nch_v, ks);
+                q.ksplit = cdiv(nch_v, q.cps);
+            }
+        }
+    };
+    grid_of(nblk);
+    if (N % 64 == 0 && t.ck == 32 && t.rt <= 3 && q.gper * q.nblk * q.ksplit < 128) {
+        q.nt1 = true;
+        grid_of(N / 32);
+    }
+    return q;
+}
+
 template <int NT, int RT, int CK, int IT = 1>
 static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p, bool bns = false) {
     constexpr bool W0 = CK == 8, W1 = CK != 16;  // the instance for wconst false / true
@@ -2012,9 +2203,19 @@ static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, cons
         hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, false, W0, IT, false>), grid, dim3(512), 0, st, p);
 }
 
+// split-K workspace bytes of an eval STORE launch (0: the shape runs unsplit)
+long long sd_halo_split_ws_bytes(const sd_src& a, int batch, int H, int W, int N, int epi, bool wsplit) {
+    const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, false);
+    int nblk, gper, nsp;
+    halo_grid(t, batch, H, W, N, nblk, gper, nsp);
+    const int nch = cdiv(a.chans[0], t.ck) + cdiv(a.chans[1], t.ck);
+    const HSplit q = halo_split_plan(t, nblk, gper, nsp, N, nch * (wsplit ? 2 : 1), epi, false);
+    return q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
+}
+
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns, bool wsplit,
-                     const float* osc, const float* osh) {
+                     const float* osc, const float* osh, void* ws, long long ws_bytes) {
     const bool st_ = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_);
     HFwdArgs p;
@@ -2054,7 +2255,21 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
         p.bmu = bns->mean;
         p.bis = bns->invstd;
     }
-    p.xcd = halo_xcd_enabled() && (p.gper * p.nblk) % 8 == 0;
+    const int nch = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck);
+    HSplit q = halo_split_plan(t, p.nblk, p.gper, p.nsp, N, nch * (wsplit ? 2 : 1), epi, bns != nullptr);
+    const long long need = q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
+    if (q.ksplit > 1 && (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0)) {  // no workspace: one group
+        q.ksplit = 1;
+        q.cps = nch * (wsplit ? 2 : 1);
+    }
+    p.nblk = q.nblk;
+    p.gper = q.gper;
+    p.gblk = q.gper * q.nblk;
+    p.ksplit = q.ksplit;
+    p.cps = q.cps;
+    p.npix = batch * H * W;
+    p.part = q.ksplit > 1 ? (float*)ws : nullptr;
+    p.xcd = halo_xcd_enabled() && (p.gblk * q.ksplit) % 8 == 0;
     p.prio = halo_prio(a);
     p.dbg = g_wg_dbg;
     const int cap = t.it == 2 ? 384 : halo_px_cap(t.rt, t.ck);
@@ -2066,11 +2281,15 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     SD_REQUIRE((long long)H * W < (1LL << 24) && (long long)H * W * (a.chans[0] > a.chans[1] ? a.chans[0] : a.chans[1]) * 2 <
                    (1LL << 31) && (long long)N * kpad * 2 < (1LL << 31) && (long long)H * W * N * 2 < (1LL << 31),
                "sd_conv_gemm(halo): image %dx%d or weights %dx%d too large for 32-bit offsets", H, W, N, kpad);
-    const dim3 grid(p.gper * p.nblk);
-    const int nch = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck);
-    const bool wc = wconst_chunks(nch * (wsplit ? 2 : 1));
+    const dim3 grid(p.gblk * q.ksplit);
+    const bool wc = wconst_chunks(q.cps);
+    SD_REQUIRE(!(N == 32 && t.ck == 32 && t.rt == 4) || (t.th == 16 && t.tw == 32),
+               "sd_conv_gemm(halo): the N = 32 RT 4 instances (vertical reuse) need 16x32 tiles, got %dx%d", t.th, t.tw);
     SD_REQUIRE(t.ck != 8 || nch == 1, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
-    if (t.ck == 8) {
+    if (q.nt1) {  // 32-channel N-blocks of an N % 64 layer (batch-1 eval)
+        if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p);
+        else launch_halo<1, 2, 32>(st_, wc, grid, st, p);
+    } else if (t.ck == 8) {
         if (t.rt == 4) launch_halo<1, 4, 8>(st_, wc, grid, st, p);
         else if (t.rt == 3) launch_halo<1, 3, 8>(st_, wc, grid, st, p);
         else launch_halo<1, 2, 8>(st_, wc, grid, st, p);
@@ -2089,6 +2308,11 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
         launch_halo<2, 3, 16>(st_, wc, grid, st, p);
     } else {
         launch_halo<2, 2, 16>(st_, wc, grid, st, p);
+    }
+    if (q.ksplit > 1) {
+        const long long n8 = (long long)batch * H * W * N / 8;
+        hipLaunchKernelGGL(k_halo_split_reduce, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, p.part, q.ksplit,
+                           n8, N, osc, osh, (__bf16*)out0);
     }
     return sd_check_launch("sd_conv_gemm(halo)");
 }

@@ -50,6 +50,13 @@ struct QArgs {
     int N, kpad, ctap;
     __bf16* out;
     int xcd;              // XCD-contiguous block numbering (grid % 8 == 0)
+    // split-K (batch-1 forwards of the deep layers, whose few items leave most CUs idle and run their chunks one after
+    // another): ksplit groups of gblk = gper * nblk blocks, group ks takes chunks [ks*cps, ks*cps + cps) of every item
+    // and stores its dequantised fp32 partial sums to part[ks][pixel][N]; k_q8_split_reduce adds the groups' partials
+    // and stores the bf16 output. ksplit = 1: no partials, the epilogue stores `out`.
+    int ksplit, gblk, cps;
+    int npix;             // batch * H * W (partials rows per split)
+    float* part;
 };
 
 // 16 bf16 channels (lo: 0-7, hi: 8-15) -> 16 e4m3 bytes: med3(y*qs + qh, lo_clamp, 448), lo_clamp = 0 for a ReLU
@@ -102,25 +109,31 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
     const bool is_loader = (tid >> 6) >= 4;
     const int wid = (tid >> 6) & 3;
     const int bid = p.xcd ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-    const int nb = bid % p.nblk, slot = bid / p.nblk;
+    const int ks = bid / p.gblk, bb = bid - ks * p.gblk;
+    const int nb = bb % p.nblk, slot = bb / p.nblk;
     const int n0 = nb * BN;
     // chunks never straddle the two sources (a source's last chunk may be partial)
     const int nc0 = (p.c0 + QC - 1) / QC;
-    const int nchunks = nc0 + (p.c1 + QC - 1) / QC;
+    const int nch_all = nc0 + (p.c1 + QC - 1) / QC;
+    const int c_lo = ks * p.cps;  // this split's chunks: [c_lo, c_lo + nchunks)
+    const int nchunks = (c_lo + p.cps < nch_all ? c_lo + p.cps : nch_all) - c_lo;
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = my_items * nchunks;
     constexpr int LS = 2;  // loader register sets
     const int padded = (total + LS - 1) / LS * LS;
     const int ctot = p.c0 + p.c1;
-    for (int c = tid; c < ctot; c += 512) {
-        const bool first = c < p.c0;
-        const int cl = first ? c : c - p.c0;
-        sq[c] = (first ? p.qs0 : p.qs1)[cl];
-        sq[QSBN + c] = (first ? p.qh0 : p.qh1)[cl];
-    }
-    if (tid < BN) deq[tid] = n0 + tid < p.N ? p.act_scale[0] * p.wscale[n0 + tid] : 0.f;
-    __syncthreads();
+    // filled by both roles before the launch's first barrier, the loaders' after they issued their first loads (one
+    // memory latency for the tables, weights and first halos: the serial latencies are what a batch-1 launch costs)
+    auto fill_tables = [&]() __attribute__((always_inline)) {
+        for (int c = tid; c < ctot; c += 512) {
+            const bool first = c < p.c0;
+            const int cl = first ? c : c - p.c0;
+            sq[c] = (first ? p.qs0 : p.qs1)[cl];
+            sq[QSBN + c] = (first ? p.qh0 : p.qh1)[cl];
+        }
+        if (tid < BN) deq[tid] = n0 + tid < p.N ? p.act_scale[0] * p.wscale[n0 + tid] : 0.f;
+    };
 
     if (is_loader) {
         // ================================================================= loader waves
@@ -175,11 +188,16 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
             else return st1;
         };
         uint4 wr[WPT];
+        // WCONST: the second chunk's weights (two chunks per item) in registers of their own, loaded with the first's
+        // (not at RT 4: its 640-pixel halo sets leave no room; there the second chunk's weights follow the barrier)
+        constexpr bool W2 = WCONST && RT != 4;
+        uint4 wr2[W2 ? WPT : 1];
         int w_cc = 0;
-        auto load_w = [&]() __attribute__((always_inline)) {  // weights of chunk w_cc -> wr, then advance
-            const bool s1 = w_cc >= nc0;
+        auto load_w_into = [&](uint4 (&wdst)[WPT]) __attribute__((always_inline)) {  // weights of chunk w_cc, advance
+            const int wc = c_lo + w_cc;
+            const bool s1 = wc >= nc0;
             const int C = s1 ? p.c1 : p.c0;
-            const int cl = (s1 ? w_cc - nc0 : w_cc) * QC;
+            const int cl = (s1 ? wc - nc0 : wc) * QC;
             if (++w_cc == nchunks) w_cc = 0;
             unsigned v[WPT];
 #pragma unroll
@@ -195,23 +213,26 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
 #pragma unroll
             for (int i = 0; i < WPT; ++i) {
                 const auto x = __builtin_amdgcn_raw_buffer_load_b128(wrs, v[i], cbg, 0);
-                wr[i] = make_uint4(x[0], x[1], x[2], x[3]);
+                wdst[i] = make_uint4(x[0], x[1], x[2], x[3]);
             }
         };
-        auto store_w = [&](int buf) __attribute__((always_inline)) {
+        auto load_w = [&]() __attribute__((always_inline)) { load_w_into(wr); };
+        auto store_w_from = [&](int buf, const uint4 (&wsrc)[WPT]) __attribute__((always_inline)) {
             uint8_t* wl = smem + buf * BUF + HALO_B;
 #pragma unroll
             for (int i = 0; i < WPT; ++i) {
                 const int item = ltid + i * 256;
                 const int co = item / (9 * QPPX), r = item - co * (9 * QPPX);
-                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * QW + r * 16) = wr[i];
+                if (item < WPIECES) *reinterpret_cast<uint4*>(wl + co * QW + r * 16) = wsrc[i];
             }
         };
+        auto store_w = [&](int buf) __attribute__((always_inline)) { store_w_from(buf, wr); };
         auto load = [&](auto S) __attribute__((always_inline)) {  // halo of chunk (ld_item, ld_cc) -> set S, advance
             HSet& q = set_of(S);
-            const bool s1 = ld_cc >= nc0;
+            const int hc = c_lo + ld_cc;
+            const bool s1 = hc >= nc0;
             const int C = s1 ? p.c1 : p.c0;
-            const int cl = (s1 ? ld_cc - nc0 : ld_cc) * QC;
+            const int cl = (s1 ? hc - nc0 : hc) * QC;
             q.cb = (s1 ? p.c0 : 0) + cl;
             q.relu = (s1 ? p.relu1 : p.relu0) != 0;
             const bool cok = cl + lpiece * 16 < C, hok = cl + lpiece * 16 + 8 < C;
@@ -274,19 +295,37 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
         };
         if (total > 0) {
             // the loads an iteration would have issued before chunk 0 (same issue order, pinned by sched barriers):
-            // the halo of chunk 0, the weights of chunk 0, the halo of chunk 1 (WCONST: weights first, stored now)
+            // the halo of chunk 0, the weights of chunk 0, the halo of chunk 1 (WCONST: the weights of both chunks
+            // first, stored after the tables)
             geometry();
             if constexpr (WCONST) {
                 load_w();  // chunk 0
-                store_w(0);
-                load_w();  // chunk 1 (chunk 0 again with one chunk per item)
-                store_w(1);
+                if constexpr (W2)
+                    if (nchunks > 1) load_w_into(wr2);  // chunk 1
+                __builtin_amdgcn_sched_barrier(0);
             }
             load(S0);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (!WCONST) load_w();
             __builtin_amdgcn_sched_barrier(0);
             load(S1);
+        }
+        fill_tables();
+        __syncthreads();  // the tables (the MFMA waves meet it before their first chunk)
+        if (total > 0) {
+            if constexpr (WCONST) {
+                store_w(0);
+                if (nchunks > 1) {
+                    if constexpr (W2) {
+                        store_w_from(1, wr2);
+                    } else {
+                        load_w();  // chunk 1
+                        store_w(1);
+                    }
+                } else {
+                    store_w(1);  // one chunk per item: chunk 0 in both buffers
+                }
+            }
             // a multiple of LS iterations: past the last chunk the loads are out of range and the stores go to a
             // buffer the MFMA waves no longer read (they meet these iterations with extra barriers)
             for (int gi = 0; gi < total; gi += LS) {
@@ -298,6 +337,8 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
     }
 
     // =============================================================== MFMA waves
+    fill_tables();
+    __syncthreads();  // the tables
     int abase[RT];  // LDS byte offset of this lane's B fragment (pixel lane & 31 of column tile i, tap (0,0))
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
@@ -373,6 +414,32 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.out + (size_t)b * hw_img * p.N), (short)0, hw_img * p.N * 2, 0x00020000);
             const int chq = 4 * (lane >> 5);
+            if (p.part) {
+                // split-K partials straight from the C layout: lane = pixel (lane & 31) of tile i, 4 consecutive
+                // channels t*32 + 8*g4 + chq + 0..3 per 16-B store (batch-1 sizes: a few MB per launch)
+                float* const pk = p.part + ((size_t)ks * p.npix + (size_t)b * hw_img) * p.N;
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    const int m = (wid + 4 * i) * 32 + (lane & 31);
+                    const int hm = m / p.tw, wm = m - hm * p.tw;
+                    const bool live = (m < mvalid) & (h0 + hm < p.H) & (w0 + wm < p.W);
+                    const size_t pix = (size_t)(h0 + hm) * p.W + w0 + wm;
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+#pragma unroll
+                        for (int g4 = 0; g4 < 4; ++g4) {
+                            const int c = t * 32 + 8 * g4 + chq;
+                            const float4 d = *reinterpret_cast<const float4*>(deq + c);
+                            if (live && n0 + c < p.N)
+                                *reinterpret_cast<float4*>(pk + pix * p.N + n0 + c) =
+                                    make_float4(acc[i][t][4 * g4] * d.x, acc[i][t][4 * g4 + 1] * d.y,
+                                                acc[i][t][4 * g4 + 2] * d.z, acc[i][t][4 * g4 + 3] * d.w);
+                        }
+                }
+                cc = 0;
+                ++item;
+                continue;
+            }
             // all tiles' scratch writes and read-backs issue back to back, then the stores: one LDS round trip per
             // item (LDS is in order per wave, so a tile's writes land after the previous tile's reads)
             uint4 rows[RT][ER];
@@ -450,6 +517,25 @@ static QTile q8_tile(int H, int W, int N, int nch) {
     return {8, 32, 2};
 }
 
+// sum of the split-K partials (part[ks][pixel][N], fp32) -> bf16 out[pixel][N]: 8 channels per thread, the splits in
+// order (deterministic)
+__global__ __launch_bounds__(256) void k_q8_split_reduce(const float* __restrict__ part, int ksplit, long long n8,
+                                                         __bf16* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const float4* src = reinterpret_cast<const float4*>(part) + 2 * i;
+    float4 a = src[0], b = src[1];
+    for (int k = 1; k < ksplit; ++k) {
+        const float4 x = src[(size_t)k * 2 * n8], y = src[(size_t)k * 2 * n8 + 1];
+        a.x += x.x, a.y += x.y, a.z += x.z, a.w += x.w;
+        b.x += y.x, b.y += y.y, b.z += y.z, b.w += y.w;
+    }
+    bf16x8 v;
+    v[0] = (__bf16)a.x, v[1] = (__bf16)a.y, v[2] = (__bf16)a.z, v[3] = (__bf16)a.w;
+    v[4] = (__bf16)b.x, v[5] = (__bf16)b.y, v[6] = (__bf16)b.z, v[7] = (__bf16)b.w;
+    reinterpret_cast<bf16x8*>(out)[i] = v;
+}
+
 template <int NT, int RT>
 static void launch_q8(bool wconst, dim3 grid, hipStream_t st, const QArgs& p) {
     if constexpr (RT == 4)
@@ -460,20 +546,72 @@ static void launch_q8(bool wconst, dim3 grid, hipStream_t st, const QArgs& p) {
         hipLaunchKernelGGL((k_halo_conv_q8<NT, RT, false>), grid, dim3(512), 0, st, p);
 }
 
+// launch plan of one conv: tile, N-blocks, blocks per N-block and the split-K groups (SD_Q8_SPLIT=0 disables the
+// split and the 32-channel N-blocks of the batch-1 shapes, for A/B runs)
+struct QPlan {
+    QTile t;
+    int nt, nblk, gper, nsp, ksplit, cps, nch;
+    bool wconst;
+};
+static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1) {
+    static const int split_env = [] {
+        const char* e = getenv("SD_Q8_SPLIT");
+        return e && *e ? atoi(e) : 1;
+    }();
+    QPlan q{};
+    q.nch = cdiv(c0, QC) + cdiv(c1, QC);
+    q.t = q8_tile(H, W, N, q.nch);
+    const long long sp = (long long)batch * cdiv(W, q.t.tw) * cdiv(H, q.t.th);
+    q.nsp = sp < (1LL << 30) ? (int)sp : (1 << 30);
+    auto grid_of = [&](int nblk) {
+        q.nblk = nblk;
+        q.gper = QPERSIST / nblk;
+        if (q.gper < 1) q.gper = 1;
+        if (q.gper > q.nsp) q.gper = q.nsp;
+        // split-K where the items leave most CUs idle: up to 256 blocks, every split at least one chunk
+        q.ksplit = 1;
+        q.cps = q.nch;
+        const int gblk = q.gper * nblk;
+        if (split_env && q.t.rt == 2 && gblk < 128 && q.nch >= 2) {
+            int ks = 256 / gblk;
+            if (ks > q.nch) ks = q.nch;
+            if (ks > 1) {
+                q.cps = cdiv(q.nch, ks);
+                q.ksplit = cdiv(q.nch, q.cps);
+            }
+        }
+    };
+    q.nt = N == 32 ? 1 : 2;
+    grid_of(N == 32 ? 1 : N / 64);
+    // 64-channel N-blocks of a few items: 32-channel ones double the blocks (the same halo is staged twice, which costs
+    // nothing while the CUs idle)
+    if (split_env && q.nt == 2 && q.t.rt == 2 && q.gper * q.nblk * q.ksplit < 128) {
+        q.nt = 1;
+        grid_of(N / 32);
+    }
+    q.wconst = q.cps <= 2;  // chunk c of every item lands in LDS buffer c: weights staged once per block
+    return q;
+}
+
 }  // namespace
 
 int sd_validate_src(const sd_src* s, const char* what);
 
-extern "C" const char* sd_conv3x3_q8_kernel_name(int H, int W, int N, int c0, int c1) {
+extern "C" const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1) {
     static thread_local char buf[64];
-    const int nch = (c0 + QC - 1) / QC + (c1 + QC - 1) / QC;
-    const QTile t = q8_tile(H, W, N, nch);
-    snprintf(buf, sizeof(buf), "k_halo_conv_q8<%d, %d, %s>", N == 32 ? 1 : 2, t.rt, nch <= 2 ? "true" : "false");
+    const QPlan q = q8_plan(batch, H, W, N, c0, c1);
+    snprintf(buf, sizeof(buf), "k_halo_conv_q8<%d, %d, %s>", q.nt, q.t.rt, q.wconst || q.t.rt == 4 ? "true" : "false");
     return buf;
 }
 
-extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
-                             const float* act_scale, int N, int kpad, void* out, sd_stream s) {
+extern "C" long long sd_conv3x3_q8_ws_bytes(int batch, int H, int W, int N, int c0, int c1) {
+    const QPlan q = q8_plan(batch, H, W, N, c0, c1);
+    return q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
+}
+
+extern "C" int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
+                                const float* act_scale, int N, int kpad, void* out, void* ws, long long ws_bytes,
+                                sd_stream s) {
     if (int e = sd_validate_src(a, "sd_conv3x3_q8")) return e;
     SD_REQUIRE(a->taps == 9 && !a->pool, "sd_conv3x3_q8: needs an unpooled 3x3 source");
     SD_REQUIRE(a->H == H && a->W == W, "sd_conv3x3_q8: source grid %dx%d != %dx%d", a->H, a->W, H, W);
@@ -491,8 +629,14 @@ extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const voi
                a->chans[0]);
     const int ctap = (ctot + 15) / 16 * 16;
     SD_REQUIRE(kpad % 64 == 0 && kpad >= 9 * ctap, "sd_conv3x3_q8: kpad %d < 9*%d", kpad, ctap);
-    const int nch = cdiv(a->chans[0], QC) + cdiv(a->chans[1], QC);
-    const QTile t = q8_tile(H, W, N, nch);
+    QPlan q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1]);
+    const long long need = q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
+    if (q.ksplit > 1 && (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0)) {  // no workspace: one group
+        q.ksplit = 1;
+        q.cps = q.nch;
+        q.wconst = q.nch <= 2;
+    }
+    const QTile t = q.t;
     QArgs p;
     p.p0 = (const __bf16*)a->ptr[0];
     p.p1 = (const __bf16*)a->ptr[1];
@@ -510,13 +654,10 @@ extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const voi
     p.tw = t.tw;
     p.tiles_x = cdiv(W, t.tw);
     p.tiles = p.tiles_x * cdiv(H, t.th);
-    p.nblk = N == 32 ? 1 : N / 64;
-    const long long sp = (long long)batch * p.tiles;
-    SD_REQUIRE(sp < (1LL << 30), "sd_conv3x3_q8: too many tiles");
-    p.nsp = (int)sp;
-    p.gper = QPERSIST / p.nblk;
-    if (p.gper < 1) p.gper = 1;
-    if (p.gper > p.nsp) p.gper = p.nsp;
+    SD_REQUIRE((long long)batch * p.tiles < (1LL << 30), "sd_conv3x3_q8: too many tiles");
+    p.nsp = q.nsp;
+    p.nblk = q.nblk;
+    p.gper = q.gper;
     p.hw = t.tw + 2;
     p.nhalo = (t.th + 2) * (t.tw + 2);
     p.wq = (const uint8_t*)wq;
@@ -526,20 +667,35 @@ extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const voi
     p.kpad = kpad;
     p.ctap = ctap;
     p.out = (__bf16*)out;
-    p.xcd = (p.gper * p.nblk) % 8 == 0;
+    p.gblk = q.gper * q.nblk;
+    p.ksplit = q.ksplit;
+    p.cps = q.cps;
+    p.npix = batch * H * W;
+    p.part = q.ksplit > 1 ? (float*)ws : nullptr;
+    const int grid_n = p.gblk * q.ksplit;
+    p.xcd = grid_n % 8 == 0;
     SD_REQUIRE(p.nhalo <= q_halo_cap(t.rt) && t.th * t.tw <= 128 * t.rt && t.th < 64 && t.tw < 512,
                "sd_conv3x3_q8: tile %dx%d", t.th, t.tw);
     // 32-bit buffer offsets: image-local pixel index (24-bit) times the channel stride, and the weights
     SD_REQUIRE((long long)H * W < (1LL << 24) && (long long)H * W * (p.c0 > p.c1 ? p.c0 : p.c1) * 2 < (1LL << 31) &&
                    (long long)N * kpad < (1LL << 31) && (long long)H * W * N * 2 < (1LL << 31),
                "sd_conv3x3_q8: image %dx%d or weights too large for 32-bit offsets", H, W);
-    const dim3 grid(p.gper * p.nblk);
-    const bool wconst = nch <= 2;  // chunk c of every item lands in LDS buffer c: weights staged once per block
-    if (N == 32) {
-        if (t.rt == 4) launch_q8<1, 4>(wconst, grid, to_stream(s), p);
-        else launch_q8<1, 2>(wconst, grid, to_stream(s), p);
+    const dim3 grid(grid_n);
+    if (q.nt == 1) {
+        if (t.rt == 4) launch_q8<1, 4>(q.wconst, grid, to_stream(s), p);
+        else launch_q8<1, 2>(q.wconst, grid, to_stream(s), p);
     } else {
-        launch_q8<2, 2>(wconst, grid, to_stream(s), p);
+        launch_q8<2, 2>(q.wconst, grid, to_stream(s), p);
+    }
+    if (q.ksplit > 1) {
+        const long long n8 = (long long)batch * H * W * N / 8;
+        hipLaunchKernelGGL(k_q8_split_reduce, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, to_stream(s), p.part,
+                           q.ksplit, n8, p.out);
     }
     return sd_check_launch("sd_conv3x3_q8");
+}
+
+extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
+                             const float* act_scale, int N, int kpad, void* out, sd_stream s) {
+    return sd_conv3x3_q8_ws(a, batch, H, W, wq, wscale, act_scale, N, kpad, out, nullptr, 0, s);
 }

@@ -374,6 +374,15 @@ class UNetEngine:
             for blk in ("enc1", "enc2", "enc3", "enc4"):
                 cl = self.convs[blk + ".1"]
                 t["pool:" + cl.name] = act(cl.level + 1, cl.cout)
+            # split-K partials of the eval convs (sd_conv3x3_ex_ws: the batch-1 shapes of the deep layers)
+            hws = 0
+            for cl in self.convs.values():
+                ch = self._fp8_src_chans(cl) + (0,)
+                dummy = L.make_src(None, ch[0], H >> cl.level, W >> cl.level, taps=9, c1=ch[1])
+                for flags in (0, L.SD_CONV_WSPLIT) if cl.off_s >= 0 else (0,):  # wsplit_eval may change later
+                    hws = max(hws, L.call("sd_conv3x3_ex_ws_bytes", dummy, B, H >> cl.level, W >> cl.level, cl.cout,
+                                          L.SD_EPI_STORE, flags))
+            t["hws"] = torch.empty(max(hws // 4, 4), dtype=f32, device=dev)
         if self.fp8:
             if train:
                 raise RuntimeError("precision='fp8' is the inference-only forward (BASELINE config 5): no training")
@@ -386,6 +395,11 @@ class UNetEngine:
                     t[f"qh{k}:{cl.name}"] = torch.empty(ch, dtype=f32, device=dev)
             t["mm:xin"] = torch.empty(L.call("sd_chan_minmax_rows", B * H * W, self.cin_pad0), self.cin_pad0, 2,
                                       dtype=f32, device=dev)
+            # split-K partials of the static-scale convs (sd_conv3x3_q8_ws: the batch-1 shapes of the deep layers)
+            q8ws = max([L.call("sd_conv3x3_q8_ws_bytes", B, H >> cl.level, W >> cl.level, cl.cout,
+                               *(self._fp8_src_chans(cl) + (0,))[:2])
+                        for cl in self.convs.values() if not self._q8_bf16(cl)] + [0])
+            t["q8ws"] = torch.empty(max(q8ws // 4, 4), dtype=f32, device=dev)
             for u in self.ups.values():
                 P = B * (H >> (u.level - 1)) * (W >> (u.level - 1))
                 t["mm:" + u.name] = torch.empty(L.call("sd_chan_minmax_rows", P, u.cout), u.cout, 2, dtype=f32,
@@ -511,9 +525,11 @@ class UNetEngine:
                        BN_EPS, mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
             zs = self.zstore and dt == L.SD_BF16 and L.call("sd_conv3x3_ex_ok", src, cl.cout) == 1
             if split or zs:
-                L.call("sd_conv3x3_ex", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s) if split else self._wp(cl.off_f),
+                hws = t["hws"]
+                L.call("sd_conv3x3_ex_ws", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s) if split else self._wp(cl.off_f),
                        cl.cout, cl.kpad_s if split else cl.kpad_f, L.SD_EPI_STORE, L.SD_CONV_WSPLIT if split else 0,
-                       scale.data_ptr() if zs else None, shift.data_ptr() if zs else None, y.data_ptr(), None, s)
+                       scale.data_ptr() if zs else None, shift.data_ptr() if zs else None, y.data_ptr(), None,
+                       hws.data_ptr(), 4 * hws.numel(), s)
                 if zs:
                     self._zs.add(cl.name)
             else:
@@ -617,9 +633,10 @@ class UNetEngine:
                    None, self._s())
             return
         _, src = self._fp8_src(cl)
-        L.call("sd_conv3x3_q8", src, ws.B, ws.H >> cl.level, ws.W >> cl.level, self.wq8.data_ptr() + cl.off8,
+        q8ws = t["q8ws"]
+        L.call("sd_conv3x3_q8_ws", src, ws.B, ws.H >> cl.level, ws.W >> cl.level, self.wq8.data_ptr() + cl.off8,
                self.wscale8.data_ptr() + 4 * cl.soff8, t["as:" + cl.name].data_ptr(), cl.cout, cl.kpad8,
-               t["y:" + cl.name].data_ptr(), self._s())
+               t["y:" + cl.name].data_ptr(), q8ws.data_ptr(), 4 * q8ws.numel(), self._s())
 
     def _forward_q8(self, ws: Workspace):
         """Static-scale fp8 forward: model state unchanged since the calibration forward (the live app's loop)."""

@@ -679,6 +679,48 @@ def _pack_split(w, ci_pad):
     return out, kpad, wd
 
 
+@pytest.mark.parametrize("H,W,c0,c1,co,wsplit,affine", [
+    (30, 40, 256, 0, 256, True, True),     # bottleneck-side 30x40 layers: 16 hi/lo chunks over 4 N-blocks
+    (15, 20, 256, 256, 512, True, True),   # decoder conv0 at 15x20: a concatenation, split across the two sources
+    (60, 80, 128, 0, 128, False, False),   # plain bf16 weights, no affine, 32-channel N-blocks
+    (15, 20, 512, 0, 512, False, True),
+])
+def test_conv3x3_ex_split_k_matches_unsplit(H, W, c0, c1, co, wsplit, affine):
+    """sd_conv3x3_ex_ws at batch 1: groups of blocks over slices of the chunks (and hi/lo passes), partials added by a
+    second launch; the same products as sd_conv3x3_ex up to fp32 summation order (within one bf16 rounding)."""
+    lib = L()
+    torch.manual_seed(11)
+    ci = c0 + c1
+    u = _nhwc(torch.randn(1, c0, H, W), "bf16")
+    sk = _nhwc(torch.randn(1, c1, H, W), "bf16") if c1 else None
+    sc, sh = (torch.rand(ci) + 0.5).to(DEV), (torch.randn(ci) * 0.2).to(DEV)
+    w = torch.randn(co, ci, 3, 3) / (3 * ci ** 0.5)
+    if wsplit:
+        wp, kpad, _ = _pack_split(w, ci)
+    else:
+        wp, kpad = _pack3(w, ci, False, "bf16")
+    src = lib.make_src(u, c0, H, W, taps=9, bn0=(sc[:c0].contiguous(), sh[:c0].contiguous()), src1=sk, c1=c1,
+                       bn1=(sc[c0:].contiguous(), sh[c0:].contiguous()) if c1 else None)
+    flags = lib.SD_CONV_WSPLIT if wsplit else 0
+    osc, osh = (torch.rand(co) + 0.5).to(DEV), torch.randn(co).to(DEV)
+    aff = (osc, osh) if affine else (None, None)
+    nbytes = lib.call("sd_conv3x3_ex_ws_bytes", src, 1, H, W, co, lib.SD_EPI_STORE, flags)
+    assert nbytes > 0, "the batch-1 deep shapes take the split-K path"
+    ws = torch.empty(nbytes // 4, device=DEV)
+    outs = []
+    for wsp in (None, ws):
+        out = torch.full((H * W, co), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lib.call("sd_conv3x3_ex_ws", src, 1, H, W, wp.data_ptr(), co, kpad, lib.SD_EPI_STORE, flags, lib.ptr(aff[0]),
+                 lib.ptr(aff[1]), out.data_ptr(), None, lib.ptr(wsp), 0 if wsp is None else 4 * ws.numel(),
+                 lib.stream_handle())
+        outs.append(out.float())
+    torch.cuda.synchronize()
+    ref, got = outs
+    assert torch.isfinite(got).all() and torch.isfinite(ref).all()
+    assert float(((got - ref).abs() - 2.0 ** -7 * ref.abs()).max()) <= 1e-6 * float(ref.abs().max())
+    assert float((got - ref).abs().mean()) <= 1e-3 * float(ref.abs().mean())
+
+
 def test_pack_conv3_split_is_hi_plus_lo():
     torch.manual_seed(7)
     w = torch.randn(32, 24, 3, 3) / 7

@@ -14,7 +14,7 @@ HEADER = Path(__file__).resolve().parents[1] / "include" / "stereo_hip.h"
 
 def _declared():
     txt = HEADER.read_text()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(sd_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long|const char\*)\s+(sd_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol():
