@@ -164,7 +164,10 @@ class GemmTimer:
             fl_tot += fl
         if not layers:
             return None
-        return {"frac_of_roofline": round(t_att / t_meas, 4), "achieved_tflops": round(fl_tot / (t_meas * 1e-3) / 1e12, 1),
+        # mfma_frac: SURVEY §8d's encoder-MFMA fraction (encoder fwd FLOPs / their kernel time / the bf16 peak), beside
+        # the per-layer roofline fraction (HBM-bound layers priced at their byte time)
+        return {"frac_of_roofline": round(t_att / t_meas, 4), "mfma_frac": round(fl_tot / (t_meas * 1e-3) / 1e12 / peak_tflops, 4),
+                "achieved_tflops": round(fl_tot / (t_meas * 1e-3) / 1e12, 1),
                 "ms_per_step": round(t_meas / steps, 4), "peak_tflops": peak_tflops, "hbm_gbs": hbm_gbs,
                 "layers": layers}
 

@@ -171,6 +171,7 @@ struct FwdArgs {
     int n_split;
     const float* bias;
     float* stats;
+    int xcd;  // 1: XCD-aware tile order (gridDim.x * gridDim.y % 8 == 0), see k_conv_fwd_bf16
 };
 
 // FA: one unpooled source tensor with 1 tap (on the grid) or 4 sub-pixel taps (at twice its resolution), K a whole
@@ -186,7 +187,18 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    // p.xcd: workgroups are dealt to the 8 XCDs round-robin in launch order (x fastest); renumbered so that each XCD
+    // owns a contiguous range of tiles with the N tiles of one M tile adjacent, the N tiles that re-read one A tile run
+    // on one XCD at about the same time and share its L2 (launch order put consecutive N tiles of an M tile on
+    // different XCDs, so each re-read went to the fabric)
+    int mt = blockIdx.x, nt = blockIdx.y;
+    if (p.xcd) {
+        const int lin = blockIdx.y * gridDim.x + blockIdx.x, tot = gridDim.x * gridDim.y;
+        const int l2 = (lin & 7) * (tot >> 3) + (lin >> 3);
+        mt = l2 / gridDim.y;
+        nt = l2 - mt * gridDim.y;
+    }
+    const int m0 = mt * BM, n0 = nt * BN;
     const int j = tid & 7, r0 = tid >> 3;
 
     // A rows owned by this thread
@@ -333,7 +345,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
                 s += red[(w * BN + tid) * 2];
                 ss += red[(w * BN + tid) * 2 + 1];
             }
-            reinterpret_cast<float2*>(p.stats)[(size_t)blockIdx.x * p.N + n0 + tid] = make_float2(s, ss);
+            reinterpret_cast<float2*>(p.stats)[(size_t)mt * p.N + n0 + tid] = make_float2(s, ss);
         }
     }
     // Stage the bf16 tile (bias added for PIXSHUF) through LDS as [row][col], then write whole 16-B
@@ -391,6 +403,7 @@ struct WgfArgs {
     int M, N;
     int pix_per_split;
     float* slab;
+    int xcd;  // 1: XCD-aware block order (grid size % 8 == 0), see k_wgrad_bf16
 };
 
 // transposed bf16 fragment with the consistent per-k-step pixel permutation of wgrad.hip
@@ -428,8 +441,22 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(const WgfArgs p) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-    const int p_begin = blockIdx.z * p.pix_per_split;
+    // p.xcd: the (M, N) tiles of one pixel split read the same pixel range of both operands (each a slice of it); in
+    // launch order they were dealt to different XCDs, so each XCD fetched the range again (4A + 2B bytes for 2 x 4
+    // tiles, measured 309 MB per launch against ~120 MB of operands). Renumbered so that each XCD owns a contiguous
+    // range of splits with all their tiles, which then share its L2.
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (p.xcd) {
+        const int gxy = gridDim.x * gridDim.y;
+        const int lin = blockIdx.z * gxy + blockIdx.y * gridDim.x + blockIdx.x, tot = gxy * gridDim.z;
+        const int l2 = (lin & 7) * (tot >> 3) + (lin >> 3);
+        bz = l2 / gxy;
+        const int r = l2 - bz * gxy;
+        by = r / gridDim.x;
+        bx = r - by * gridDim.x;
+    }
+    const int m0 = bx * BM, n0 = by * BN;
+    const int p_begin = bz * p.pix_per_split;
     const int p_end = min(p.P, p_begin + p.pix_per_split);
     const int ntiles = p_end > p_begin ? (p_end - p_begin + BKP - 1) / BKP : 0;
 
@@ -545,7 +572,7 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(const WgfArgs p) {
         __syncthreads();
     }
 
-    float* slab = p.slab + (size_t)blockIdx.z * p.M * p.N;
+    float* slab = p.slab + (size_t)bz * p.M * p.N;
     const int ccol = lane & 15, crow = (lane >> 4) * 4;
 #pragma unroll
     for (int i = 0; i < RM; ++i)
@@ -688,6 +715,11 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
     p.stats = stats;
     const FCfg c = pick_fwd(M, N);
     dim3 grid(cdiv(M, c.bm), cdiv(N, c.bn));
+    static const bool xcd_env = [] {
+        const char* e = getenv("SD_FAST_XCD");
+        return !(e && atoi(e) == 0);
+    }();
+    p.xcd = xcd_env && grid.y > 1 && (grid.x * grid.y) % 8 == 0;
     const bool fa = ffa_shape(a) && p.a.kchunks % FKC == 0 && (long long)M * (a.taps == 4 ? 4 : 1) * a.chans[0] < (1LL << 31);
     if (fa) {
         if (c.bn == 32)
@@ -725,6 +757,11 @@ int sd_fast_wgrad_gemm(const sd_src& a, const sd_src& b, int batch, int H, int W
     p.slab = slab;
     const FCfg c = pick_wg(M, N);
     dim3 grid(cdiv(M, c.bm), cdiv(N, c.bn), splits);
+    static const bool xcd_env = [] {
+        const char* e = getenv("SD_FAST_XCD");
+        return !(e && atoi(e) == 0);
+    }();
+    p.xcd = xcd_env && (grid.x * grid.y * grid.z) % 8 == 0;
     // ConvTranspose2d shape: one 1x1 source without a pool, a 4-tap sub-pixel source of one tensor, 32-bit offsets
     const bool ct = fwg_ct_shape(a, b) && a.H == H && a.W == W && (long long)p.P * a.chans[0] < (1LL << 31) &&
                     4LL * p.P * b.chans[0] < (1LL << 31);

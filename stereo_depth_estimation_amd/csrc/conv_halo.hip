@@ -235,6 +235,10 @@ struct HFwdArgs {
 #ifndef HC_ST_AUX
 #define HC_ST_AUX 2
 #endif
+// the vertical-reuse k-loop of the N = 32 RT = 4 conv instances (k_halo_conv); HC_VR=0 builds: the per-tap loop
+#ifndef HC_VR
+#define HC_VR 1
+#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // BN statistics of one stored 16-B piece (8 bf16 channels; a pixel outside the tile adds zeros): channel pair q's
 // (sum, sum) in own[4q + {0,1}] and (sumsq, sumsq) in own[4q + {2,3}], so each pair is one v_pk_add_f32 and one
@@ -690,9 +694,6 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // column kw meet the same halo fragments one row apart, so each 16-pixel halo fragment (row hr, half h, shifted by
     // kw) is read once and feeds the up-to-3 output rows hr - kh: (RT + 2) x 2 reads per kw instead of 3 x 2RT, 40 %
     // fewer of the LDS fragment reads that paced the full-resolution layers' MFMA phase. HC_VR=0 builds: the per-tap loop.
-#ifndef HC_VR
-#define HC_VR 1
-#endif
     constexpr bool VR = HC_VR && M16 && NT == 1 && RT == 4;
     // B-fragment (pixel) halo offsets of this lane's columns (tap (0,0)), the same for every tile;
     // columns past the tile read pixel 0 and are masked in the epilogue
@@ -857,7 +858,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         auto read_frags = [&](int step) {
             const int slot_ = step % (PF + 1);
             // CK 8: a k-step is two taps of 8 channels (lane half = tap parity); tap 9 is padding
-            const int tapv = CK == 8 ? 2 * step + (lane >> 5) : step / (CK >= 16 ? CK / 16 : 1);
+            // the N = 32 RT = 4 BNS dgrads take the taps kernel-column-major (0, 3, 6, 1, ...), the order in which
+            // the vertical-reuse k-loop of the same shape's STORE instance accumulates them: identical fp32 sums
+            const int tj = step / (CK >= 16 ? CK / 16 : 1);
+            const int tapv = CK == 8 ? 2 * step + (lane >> 5) : (HC_VR && NT == 1 && RT == 4 ? (tj % 3) * 3 + tj / 3 : tj);
             const int tap = tapv < 9 ? tapv : 8;
             const int c8 = CK == 8 ? 0 : (step % (CK >= 16 ? CK / 16 : 1)) * 2 + (lane >> 5);  // 8-channel piece
             const int toff = (tap / 3) * p.hw + tap % 3;

@@ -599,12 +599,14 @@ int sd_validate_src(const sd_src* s, const char* what);
 
 extern "C" const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1) {
     static thread_local char buf[64];
+    if (batch <= 0 || H <= 0 || W <= 0 || !(N == 32 || (N > 0 && N % 64 == 0)) || c0 <= 0 || c1 < 0) return "";
     const QPlan q = q8_plan(batch, H, W, N, c0, c1);
     snprintf(buf, sizeof(buf), "k_halo_conv_q8<%d, %d, %s>", q.nt, q.t.rt, q.wconst || q.t.rt == 4 ? "true" : "false");
     return buf;
 }
 
 extern "C" long long sd_conv3x3_q8_ws_bytes(int batch, int H, int W, int N, int c0, int c1) {
+    if (batch <= 0 || H <= 0 || W <= 0 || !(N == 32 || (N > 0 && N % 64 == 0)) || c0 <= 0 || c1 < 0) return 0;
     const QPlan q = q8_plan(batch, H, W, N, c0, c1);
     return q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
 }

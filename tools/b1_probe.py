@@ -1,4 +1,4 @@
-"""Per-launch cost of the eval convs at batch 1 (the live app's forward), inside a HIP graph.
+"""Per-launch cost of the eval convs at batch 1, 960x720 (the live app's forward), inside a HIP graph.
 
     python tools/b1_probe.py [reps]
 
@@ -17,14 +17,14 @@ import torch  # noqa: E402
 
 from stereo_depth_estimation_amd import _lib as L  # noqa: E402
 
-SHAPES = [  # (H, W, cin, cout)
+SHAPES = [  # (H, W, cin, cout): the live app's 960x720 forward, one shape per U-Net level
     (16, 32, 32, 32),
-    (240, 320, 32, 32),
-    (120, 160, 64, 64),
-    (60, 80, 128, 128),
-    (30, 40, 256, 256),
-    (30, 40, 512, 256),
-    (15, 20, 512, 512),
+    (720, 960, 32, 32),
+    (360, 480, 64, 64),
+    (180, 240, 128, 128),
+    (90, 120, 256, 256),
+    (90, 120, 512, 256),
+    (45, 60, 512, 512),
 ]
 
 
@@ -60,7 +60,7 @@ def main() -> None:
     t = torch.zeros(1, device=dev)
     print(f"torch add (1 element): {graph_time(lambda: t.add_(1.0), reps, s):7.2f} us")
     # chained full-resolution pair (enc1.0 -> enc1.1): singles vs the pair in one graph
-    H, W = 240, 320
+    H, W = 720, 960
     x8 = torch.randn(H * W, 8, device=dev).to(torch.bfloat16)
     w1 = (torch.randn(32 * 128, device=dev) * 0.05).to(torch.bfloat16)
     w2 = (torch.randn(32 * 320, device=dev) * 0.05).to(torch.bfloat16)
