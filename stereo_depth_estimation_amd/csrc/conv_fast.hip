@@ -177,13 +177,18 @@ struct FwdArgs {
 // FA: one unpooled source tensor with 1 tap (on the grid) or 4 sub-pixel taps (at twice its resolution), K a whole
 // number of 64-wide tiles, 32-bit offsets: each row's base offset is computed once and a K tile adds the tap's
 // constant offset (the general gather's per-load tap test and 64-bit address math paced the ConvTranspose GEMMs)
-template <int BM, int BN, int WM, int WN, bool FA>
+// NBUF = 1: one LDS buffer (load k-tile t+1 into registers, MFMAs on t, barrier, store t+1, barrier): 24 KB at 64 x 128,
+// six blocks per CU instead of three, so other blocks' MFMAs cover each block's load latency. The 64 x 128 FA tiles
+// run the ConvTranspose layers at 15x20..30x40 (up1 forward, up3/up4 dgrad: K = 512-1024 over 300-1200 M tiles), where
+// one block's k-tile is 16 MFMAs against a 1-2 us load: latency at three blocks per CU, not bandwidth.
+template <int BM, int BN, int WM, int WN, bool FA, int NBUF = 2>
 __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
     constexpr int WTM = BM / WM, WTN = BN / WN, RM = WTM / 16, RN = WTN / 16;
     constexpr int AR = BM / 32, BR = (BN + 31) / 32;  // rows per thread (8 chunks per row, 32 rows per pass)
     static_assert(WM * WN == 4, "4 waves");
+    static_assert(NBUF == 1 || NBUF == 2, "one or two LDS buffers");
     constexpr int ABUF = BM * FBK, BBUF = BN * FBK;
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (ABUF + BBUF)];
+    __shared__ __attribute__((aligned(16))) __bf16 smem[NBUF * (ABUF + BBUF)];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
@@ -287,7 +292,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
     store_tile(0);
     __syncthreads();
     for (int kt = 0; kt < p.ktiles; ++kt) {
-        const int buf = kt & 1;
+        const int buf = NBUF == 2 ? kt & 1 : 0;
         if (kt + 1 < p.ktiles) load_tile(kt + 1);
         const __bf16* As = smem + buf * (ABUF + BBUF);
         const __bf16* Bs = As + ABUF;
@@ -306,7 +311,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
                 for (int jj = 0; jj < RN; ++jj)
                     acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[jj], acc[i][jj], 0, 0, 0);
         }
-        if (kt + 1 < p.ktiles) store_tile(buf ^ 1);
+        if constexpr (NBUF == 1) __syncthreads();  // every wave is done reading the one buffer
+        if (kt + 1 < p.ktiles) store_tile(NBUF == 2 ? buf ^ 1 : 0);
         __syncthreads();
     }
 
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
     // Stage the bf16 tile (bias added for PIXSHUF) through LDS as [row][col], then write whole 16-B
     // pieces: rows of the NHWC output, SPLIT halves, or the 2x2 sub-pixel scatter of a convT.
     constexpr int OLD = BN + 8;
-    static_assert(BM * OLD <= 2 * (ABUF + BBUF), "epilogue staging fits");
+    static_assert(BM * OLD <= NBUF * (ABUF + BBUF), "epilogue staging fits");
     __syncthreads();  // the STATS reduction and the last k-tile are done with smem
     __bf16* st = smem;
     const int C4 = p.N >> 2;
@@ -427,6 +433,8 @@ __device__ __forceinline__ bf16x8 frag_tr64(const __bf16* lds, int ld, int col0,
 // twice its resolution). Pixel m = r*W + w of the grid reads A at m*Ca and B at (4*r*W + 2*w + toff)*Cb with 32-bit
 // element offsets: one division per B load instead of two per load plus the general tap test (the loader's VALU,
 // ~240 per 64-pixel tile per lane in the general form, paced these layers at ~300 TFLOP/s)
+// (A single-buffered form at twice the resident blocks per CU, as k_conv_fwd_bf16's NBUF = 1, measured no faster here:
+// 49.8-51.0 vs 50.3-50.4 us at 128 x 128, 87.1-87.5 vs 86.7-87.2 us at 64 x 128; same box, two rounds.)
 template <int BM, int BN, int WM, int WN, bool CT>
 __global__ __launch_bounds__(256) void k_wgrad_bf16(const WgfArgs p) {
     constexpr int BKP = 64;
@@ -650,10 +658,15 @@ static bool ffa_shape(const sd_src& a) {
 // ---------------------------------------------------------------------- host dispatch (bf16)
 int sd_fast_fwd_rows(long long M, int N) { return cdiv(M, pick_fwd(M, N).bm); }
 
+static int fwd_nbuf();
+
 const char* sd_fast_fwd_name(const sd_src& a, long long M, int N) {
     static thread_local char buf[96];
     const FCfg c = pick_fwd(M, N);
-    snprintf(buf, sizeof(buf), "k_conv_fwd_bf16<%d, %d, %d, %d, %s>", c.bm, c.bn, c.wm, c.wn, ffa_shape(a) ? "true" : "false");
+    const bool fa = ffa_shape(a);
+    const bool one = fa && c.bm == 64 && c.bn == 128 && fwd_nbuf() == 1;  // the single-buffered instance
+    snprintf(buf, sizeof(buf), "k_conv_fwd_bf16<%d, %d, %d, %d, %s%s>", c.bm, c.bn, c.wm, c.wn, fa ? "true" : "false",
+             one ? ", 1" : "");
     return buf;
 }
 
@@ -693,6 +706,15 @@ int sd_fast_wgrad_splits(long long P, int M, int N) {
     return (int)splits;
 }
 
+// SD_FAST_NBUF=2: the double-buffered 64 x 128 FA tiles (A/B runs)
+static int fwd_nbuf() {
+    static const int v = [] {
+        const char* e = getenv("SD_FAST_NBUF");
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
+
 int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                       void* out1, int n_split, const float* bias, float* stats, hipStream_t st) {
     const long long M = (long long)batch * H * W;
@@ -728,6 +750,8 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
             hipLaunchKernelGGL((k_conv_fwd_bf16<128, 64, 2, 2, true>), grid, dim3(256), 0, st, p);
         else if (c.bm == 128)
             hipLaunchKernelGGL((k_conv_fwd_bf16<128, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
+        else if (fwd_nbuf() == 1)
+            hipLaunchKernelGGL((k_conv_fwd_bf16<64, 128, 2, 2, true, 1>), grid, dim3(256), 0, st, p);
         else
             hipLaunchKernelGGL((k_conv_fwd_bf16<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
     } else if (c.bn == 32)

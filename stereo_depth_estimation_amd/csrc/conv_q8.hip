@@ -546,18 +546,18 @@ static void launch_q8(bool wconst, dim3 grid, hipStream_t st, const QArgs& p) {
         hipLaunchKernelGGL((k_halo_conv_q8<NT, RT, false>), grid, dim3(512), 0, st, p);
 }
 
-// launch plan of one conv: tile, N-blocks, blocks per N-block and the split-K groups (SD_Q8_SPLIT=0 disables the
-// split and the 32-channel N-blocks of the batch-1 shapes, for A/B runs)
+// launch plan of one conv: tile, N-blocks, blocks per N-block and (split = true) the split-K groups and 32-channel
+// N-blocks of a grid of fewer than 128 blocks. The engine passes no workspace by default (SD_Q8_SPLIT=1 in the engine
+// does): at the live app's 960x720 only the 45x60 bottleneck convs qualify, and their split (2 groups, 192 blocks) saved
+// 4.8 us of kernel against the 5.0 us of the reduce launch (bottleneck.1 30.9 -> 26.1 + 5.0 us, bottleneck.0 19.3 ->
+// 17.0 + 5.0 us). The e4m3 chunks hold 64 channels, so these layers have 4-8 chunks per item against the bf16 path's
+// 16-32 (hi/lo passes of 32-channel chunks), where the same split pays (sd_conv3x3_ex_ws).
 struct QPlan {
     QTile t;
     int nt, nblk, gper, nsp, ksplit, cps, nch;
     bool wconst;
 };
-static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1) {
-    static const int split_env = [] {
-        const char* e = getenv("SD_Q8_SPLIT");
-        return e && *e ? atoi(e) : 1;
-    }();
+static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1, bool split) {
     QPlan q{};
     q.nch = cdiv(c0, QC) + cdiv(c1, QC);
     q.t = q8_tile(H, W, N, q.nch);
@@ -568,11 +568,10 @@ static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1) {
         q.gper = QPERSIST / nblk;
         if (q.gper < 1) q.gper = 1;
         if (q.gper > q.nsp) q.gper = q.nsp;
-        // split-K where the items leave most CUs idle: up to 256 blocks, every split at least one chunk
         q.ksplit = 1;
         q.cps = q.nch;
         const int gblk = q.gper * nblk;
-        if (split_env && q.t.rt == 2 && gblk < 128 && q.nch >= 2) {
+        if (split && q.t.rt == 2 && gblk < 128 && q.nch >= 2) {  // up to 256 blocks, every split >= 1 chunk
             int ks = 256 / gblk;
             if (ks > q.nch) ks = q.nch;
             if (ks > 1) {
@@ -583,9 +582,8 @@ static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1) {
     };
     q.nt = N == 32 ? 1 : 2;
     grid_of(N == 32 ? 1 : N / 64);
-    // 64-channel N-blocks of a few items: 32-channel ones double the blocks (the same halo is staged twice, which costs
-    // nothing while the CUs idle)
-    if (split_env && q.nt == 2 && q.t.rt == 2 && q.gper * q.nblk * q.ksplit < 128) {
+    // 64-channel N-blocks of a few items: 32-channel ones double the blocks
+    if (split && q.nt == 2 && q.t.rt == 2 && q.gper * q.nblk * q.ksplit < 128) {
         q.nt = 1;
         grid_of(N / 32);
     }
@@ -600,14 +598,14 @@ int sd_validate_src(const sd_src* s, const char* what);
 extern "C" const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1) {
     static thread_local char buf[64];
     if (batch <= 0 || H <= 0 || W <= 0 || !(N == 32 || (N > 0 && N % 64 == 0)) || c0 <= 0 || c1 < 0) return "";
-    const QPlan q = q8_plan(batch, H, W, N, c0, c1);
+    const QPlan q = q8_plan(batch, H, W, N, c0, c1, false);
     snprintf(buf, sizeof(buf), "k_halo_conv_q8<%d, %d, %s>", q.nt, q.t.rt, q.wconst || q.t.rt == 4 ? "true" : "false");
     return buf;
 }
 
 extern "C" long long sd_conv3x3_q8_ws_bytes(int batch, int H, int W, int N, int c0, int c1) {
     if (batch <= 0 || H <= 0 || W <= 0 || !(N == 32 || (N > 0 && N % 64 == 0)) || c0 <= 0 || c1 < 0) return 0;
-    const QPlan q = q8_plan(batch, H, W, N, c0, c1);
+    const QPlan q = q8_plan(batch, H, W, N, c0, c1, true);
     return q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
 }
 
@@ -631,13 +629,10 @@ extern "C" int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const 
                a->chans[0]);
     const int ctap = (ctot + 15) / 16 * 16;
     SD_REQUIRE(kpad % 64 == 0 && kpad >= 9 * ctap, "sd_conv3x3_q8: kpad %d < 9*%d", kpad, ctap);
-    QPlan q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1]);
+    QPlan q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1], true);
     const long long need = q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
-    if (q.ksplit > 1 && (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0)) {  // no workspace: one group
-        q.ksplit = 1;
-        q.cps = q.nch;
-        q.wconst = q.nch <= 2;
-    }
+    if (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0)  // no (or too small a) workspace: the unsplit plan
+        q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1], false);
     const QTile t = q.t;
     QArgs p;
     p.p0 = (const __bf16*)a->ptr[0];
