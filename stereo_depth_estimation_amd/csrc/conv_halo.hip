@@ -329,6 +329,8 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     // (Tried: 512-pixel items, NT = 2 x RT = 4 at 12x32 / 10x40 tiles with a 512-pixel halo, to halve the weight
     // staging per MFMA: 10-30 % slower per layer. Those tiles hold 384-400 pixels, so a quarter of the MFMA columns
     // idle, and the 128 accumulators leave no room for a fragment ring.)
+    // (Also with the vertical-reuse k-loop's smaller fragment ring, 48 VGPRs instead of 80, the N = 32 RT = 4 BNS dgrad
+    // spills 75-122 VGPRs in this form: its y pieces, BatchNorm constants and sums sit beside the accumulators.)
     constexpr bool M16 = CK == 32 && IT == 1 && !BNS;
     constexpr int HX_LD = halo_ld(CK), W_LD = M16 ? 9 * CK : wrow_ld(CK);
     constexpr int HPX = IT == 2 ? 384 : halo_px_cap(RT, CK);  // IT = 2: the CK = 32 tilings (halo <= 384 px)
@@ -689,7 +691,10 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
     __syncthreads();  // the tables
     // 32-pixel column tile i of this MFMA wave: the M16 instances own RT consecutive ones (in 32-pixel-wide tiles, RT
     // consecutive rows: what the vertical-reuse k-loop below needs), the others every fourth
-    auto tile_T = [&](int i) { return M16 ? wid * RT + i : wid + 4 * i; };
+    // The N = 32 RT = 4 BNS dgrads (32x32x16 MFMAs, VR32) run the same vertical reuse on 32-pixel fragments (one tile row
+    // each) and channel halves, in the tap order of the 16x16x32 loop (so their stores equal the STORE instance's)
+    constexpr bool VR32 = HC_VR && !M16 && NT == 1 && RT == 4 && CK == 32 && IT == 1;
+    auto tile_T = [&](int i) { return M16 || VR32 ? wid * RT + i : wid + 4 * i; };
     // Vertical reuse (the N = 32 RT = 4 instances: full-resolution 16x32 tiles, 4 rows per wave): the taps of one kernel
     // column kw meet the same halo fragments one row apart, so each 16-pixel halo fragment (row hr, half h, shifted by
     // kw) is read once and feeds the up-to-3 output rows hr - kh: (RT + 2) x 2 reads per kw instead of 3 x 2RT, 40 %
@@ -858,10 +863,7 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
         auto read_frags = [&](int step) {
             const int slot_ = step % (PF + 1);
             // CK 8: a k-step is two taps of 8 channels (lane half = tap parity); tap 9 is padding
-            // the N = 32 RT = 4 BNS dgrads take the taps kernel-column-major (0, 3, 6, 1, ...), the order in which
-            // the vertical-reuse k-loop of the same shape's STORE instance accumulates them: identical fp32 sums
-            const int tj = step / (CK >= 16 ? CK / 16 : 1);
-            const int tapv = CK == 8 ? 2 * step + (lane >> 5) : (HC_VR && NT == 1 && RT == 4 ? (tj % 3) * 3 + tj / 3 : tj);
+            const int tapv = CK == 8 ? 2 * step + (lane >> 5) : step / (CK >= 16 ? CK / 16 : 1);
             const int tap = tapv < 9 ? tapv : 8;
             const int c8 = CK == 8 ? 0 : (step % (CK >= 16 ? CK / 16 : 1)) * 2 + (lane >> 5);  // 8-channel piece
             const int toff = (tap / 3) * p.hw + tap % 3;
@@ -955,6 +957,46 @@ __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
                 __builtin_amdgcn_sched_barrier(0);
             }
           }
+        } else if (VR32 && !(WG_EXP & 8)) {
+            // steps (kw, halo row hr, channel half ch); weights of (kh, kw, ch) in one set: column kw+1's kh = 0, 1 are
+            // read during column kw's last row (kh = 2 only), its kh = 2 during its own first row (kh = 0 only)
+            constexpr int R = RT, NH = R + 2, NS = 3 * NH * 2, PV = 2, HWV = 34;
+            bf16x8 av[3][2];
+            bf16x8 xv[PV + 1];
+            const __bf16* const xb = hx + (wid * RT * HWV + (lane & 31)) * HX_LD + (lane >> 5) * 8;
+            auto readA = [&](int kw, int kh) __attribute__((always_inline)) {
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch)
+                    av[kh][ch] = *reinterpret_cast<const bf16x8*>(wl + (lane & 31) * W_LD + (kh * 3 + kw) * CK +
+                                                                  (ch * 2 + (lane >> 5)) * 8);
+            };
+            auto readX = [&](int st) __attribute__((always_inline)) {
+                const int kw = st / (2 * NH), hr = (st >> 1) % NH, ch = st & 1;
+                xv[st % (PV + 1)] = *reinterpret_cast<const bf16x8*>(xb + (hr * HWV + kw) * HX_LD + ch * 16);
+            };
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) readA(0, kh);
+#pragma unroll
+            for (int st = 0; st < PV; ++st) readX(st);
+#pragma unroll
+            for (int st = 0; st < NS; ++st) {
+                const int kw = st / (2 * NH), hr = (st >> 1) % NH, ch = st & 1;
+                if (hr == NH - 1 && ch == 0 && kw < 2) {
+                    readA(kw + 1, 0);
+                    readA(kw + 1, 1);
+                }
+                if (hr == 0 && ch == 0 && kw > 0) readA(kw, 2);
+                if (st + PV < NS) readX(st + PV);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    const int r = hr - kh;
+                    if (r < 0 || r >= R) continue;
+                    acc[0][r][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[kh][ch], xv[st % (PV + 1)], acc[0][r][0], 0,
+                                                                           0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
         } else if (!(WG_EXP & 8)) {
 #pragma unroll
         for (int step = 0; step < PF; ++step) read_frags(step);

@@ -35,6 +35,8 @@ LAYERS = [  # (H, W, cin, cout, stats)
     (30, 40, 512, 256, True),    # dec4.0
     (15, 20, 256, 512, True),
     (15, 20, 512, 512, True),
+    (240, 320, 32, 32, "bns"),   # enc1.1 / dec1.1 dgrad with the fused BatchNorm-backward sums (sd_conv_gemm_bnsum)
+    (120, 160, 64, 64, "bns"),
 ]
 
 
@@ -46,12 +48,23 @@ def run(B, H, W, ci, co, stats, s, dev, n=20):
     kpad = ((9 * ci + 63) // 64) * 64
     w = (torch.randn(co * kpad, device=dev) * 0.05).to(torch.bfloat16)
     o = torch.empty(B * H * W, co, device=dev, dtype=torch.bfloat16)
+    bns = stats == "bns"
+    stats = stats is True
     epi = L.SD_EPI_STATS if stats else L.SD_EPI_STORE
     src = L.make_src(y, ci, H, W, taps=9, bn0=(sc, sh) if stats else None)
-    rows = L.call("sd_conv_gemm_stat_rows", L.SD_BF16, B, H, W, co)
+    rows = L.call("sd_conv_gemm_bnsum_rows", src, B, H, W, co) if bns else L.call("sd_conv_gemm_stat_rows",
+                                                                                  L.SD_BF16, B, H, W, co)
     st = torch.zeros(rows * co * 2, device=dev)
+    if bns:  # the BatchNorm layer whose upstream gradient this dgrad stores: its raw output and constants
+        yb = torch.randn(B * H * W, co, device=dev).to(torch.bfloat16)
+        bsc, bsh = torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev) * 0.1
+        bmu, bis = torch.randn(co, device=dev) * 0.1, torch.rand(co, device=dev) + 0.5
 
     def once():
+        if bns:
+            L.call("sd_conv_gemm_bnsum", L.SD_BF16, src, B, H, W, w.data_ptr(), co, kpad, o.data_ptr(), yb.data_ptr(),
+                   bsc.data_ptr(), bsh.data_ptr(), bmu.data_ptr(), bis.data_ptr(), st.data_ptr(), s)
+            return
         L.call("sd_conv_gemm", L.SD_BF16, src, B, H, W, w.data_ptr(), co, kpad, epi, o.data_ptr(),
                None, 0, None, st.data_ptr() if stats else None, s)
 
@@ -65,7 +78,7 @@ def run(B, H, W, ci, co, stats, s, dev, n=20):
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1000 / n
-    name = L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, B, H, W, co, epi)
+    name = L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, B, H, W, co, epi) + (" bns" if bns else "")
     if os.environ.get("SD_WG_DIAG"):  # per-wave cycle counters of a -DWG_EXP=1024 build
         dbg = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device=dev)
         L.call("sd_debug_buffer", dbg.data_ptr())
@@ -162,7 +175,7 @@ def main():
             rounds = int(a.split("=", 1)[1])
     for H, W, ci, co, stats in LAYERS:
         flops = 2.0 * B * H * W * co * 9 * ci
-        line = f"{H}x{W} {ci}->{co} {'fwd ' if stats else 'dgrd'}"
+        line = f"{H}x{W} {ci}->{co} {'bns ' if stats == 'bns' else 'fwd ' if stats else 'dgrd'}"
         ref = None
         best = {}
         for _ in range(rounds):
