@@ -229,7 +229,9 @@ def pmc_traffic(kernel: str):
     sha = lib_sha256()
     if d.get("lib_sha256") != sha:
         return None, f"profiles/pmc_traffic.json is from another build ({str(d.get('lib_sha256'))[:12]} != {sha[:12]})"
-    k = d.get("kernels", {}).get(kernel)
+    ks = d.get("kernels", {})
+    # rocprofv3 names every template argument; the library's names leave out trailing defaults (k_halo_conv's OAFF)
+    k = ks.get(kernel) or ks.get(kernel[:-1] + ", false>")
     if k is None:
         return None, "kernel not in profiles/pmc_traffic.json"
     return k.get("hbm_bytes_per_launch"), f"profiles/pmc_traffic.json (same build, {sha[:12]})"
