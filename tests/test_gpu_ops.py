@@ -899,3 +899,27 @@ def test_conv3x3_weights_in_registers_equal_lds_weights(monkeypatch, B, H, W, c0
     for st in (st1, st0):
         assert torch.allclose(st[:, 0], g64.sum((0, 2, 3)), rtol=1e-5, atol=1e-3)
         assert torch.allclose(st[:, 1], (g64 * g64).sum((0, 2, 3)), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,C,H,W", [(3, 6, 24, 32), (2, 7, 10, 14), (1, 6, 5, 7), (2, 8, 16, 20)])
+def test_pack_input_nchw_to_padded_nhwc(prec, B, C, H, W):
+    """sd_pack_input / sd_pack_input_amax: NCHW fp32 -> NHWC with the channels zero-padded to 8, in the path's dtype
+    (the four-pixel form where H*W % 4 == 0, the per-pixel form otherwise); the amax form also takes max |x| into its
+    slot and clears another."""
+    lib = L()
+    torch.manual_seed(17)
+    x = (torch.randn(B, C, H, W) * 3).to(DEV)
+    ref = torch.zeros(B, H, W, 8)
+    ref[..., :C] = x.cpu().permute(0, 2, 3, 1)
+    ref = ref.to(_adt(prec)).reshape(B * H * W, 8)
+    s = lib.stream_handle()
+    out = torch.full((B * H * W, 8), float("nan"), dtype=_adt(prec), device=DEV)
+    lib.call("sd_pack_input", _sd(prec), x.data_ptr(), B, C, H, W, 8, out.data_ptr(), s)
+    amax = torch.tensor([0, 12345], dtype=torch.int32, device=DEV)
+    out2 = torch.full_like(out, float("nan"))
+    lib.call("sd_pack_input_amax", _sd(prec), x.data_ptr(), B, C, H, W, 8, out2.data_ptr(), amax.data_ptr(), 0, 1, s)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref) and torch.equal(out2.cpu(), ref)
+    got_max = amax[:1].cpu().view(torch.float32).item()
+    assert got_max == float(x.abs().max()) and int(amax[1]) == 0
