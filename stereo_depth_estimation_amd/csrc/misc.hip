@@ -85,45 +85,6 @@ __global__ __launch_bounds__(256) void k_pack_input_amax(const float* __restrict
     if (blockIdx.x == 0 && threadIdx.x == 64 && clear >= 0) amax[clear] = 0u;
 }
 
-// the common case of both packs (cpad == 8, H*W % 4 == 0, 16-B aligned planes): four consecutive pixels per thread, one
-// 16-B load per channel plane and four 16-B (bf16) stores, 32-bit index math; r04: k_pack_input read its 6 planes with
-// 4-B loads and 64-bit per-pixel divisions (48 us per step at 4.1 TB/s)
-template <typename T, bool AMAX>
-__global__ __launch_bounds__(256) void k_pack_input4(const float* __restrict__ x, int cin, unsigned hw, unsigned quads,
-                                                     T* __restrict__ out, unsigned* amax, int slot, int clear) {
-    const unsigned hq = hw >> 2;
-    float m = 0.f;
-    for (unsigned q = blockIdx.x * 256u + threadIdx.x; q < quads; q += gridDim.x * 256u) {
-        const unsigned b = q / hq, r = (q - b * hq) * 4u;
-        const float* src = x + (size_t)b * cin * hw + r;
-        float v[4][8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float4 f = c < cin ? *reinterpret_cast<const float4*>(src + (size_t)c * hw) : make_float4(0.f, 0.f, 0.f, 0.f);
-            v[0][c] = f.x;
-            v[1][c] = f.y;
-            v[2][c] = f.z;
-            v[3][c] = f.w;
-            if (AMAX) m = fmaxf(m, fmaxf(fmaxf(fabsf(f.x), fabsf(f.y)), fmaxf(fabsf(f.z), fabsf(f.w))));
-        }
-        T* o = out + (size_t)q * 32;  // pixel 4q, 8 channels each
-#pragma unroll
-        for (int p = 0; p < 4; ++p) store8(o + p * 8, v[p]);
-    }
-    if constexpr (AMAX) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        __shared__ float wm[4];
-        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
-        __syncthreads();
-        if (threadIdx.x == 0) {  // as k_pack_input_amax
-            const unsigned mb = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
-            if (mb > __hip_atomic_load(amax + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(amax + slot, mb);
-        }
-        if (blockIdx.x == 0 && threadIdx.x == 64 && clear >= 0) amax[clear] = 0u;
-    }
-}
-
 // fwd : out[o][tap*ci_pad + i] = w[o][i][tap]
 // dgrad: out[i][tap*co + o]    = w[o][i][8 - tap]
 template <typename T>
@@ -332,12 +293,6 @@ __global__ void k_resize_bilinear(const float* __restrict__ in, int planes, int 
     }
 }
 
-// k_pack_input4's shape: 8 packed channels, whole pixel quads per image, 16-B aligned planes, 32-bit pixel indices
-bool pack4_ok(const float* x, int batch, int cin, int H, int W, int cpad) {
-    return cpad == 8 && cin <= 8 && ((long long)H * W) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
-           (long long)batch * H * W < (1LL << 32) && (long long)H * W < (1LL << 30);
-}
-
 int grid_for(long long work) {
     long long g = (work + 255) / 256;
     if (g > 8192) g = 8192;
@@ -350,17 +305,6 @@ extern "C" int sd_pack_input(int dtype, const float* x, int batch, int cin, int 
                              sd_stream s) {
     SD_REQUIRE(x && out && batch > 0 && cin > 0 && H > 0 && W > 0, "sd_pack_input: bad args");
     SD_REQUIRE(cpad >= cin && cpad % 8 == 0, "sd_pack_input: cpad %d", cpad);
-    if (pack4_ok(x, batch, cin, H, W, cpad)) {
-        const unsigned quads = (unsigned)((long long)batch * H * W / 4);
-        const int g4 = grid_for(quads);
-        if (dtype == SD_BF16)
-            hipLaunchKernelGGL((k_pack_input4<__bf16, false>), dim3(g4), dim3(256), 0, to_stream(s), x, cin,
-                               (unsigned)(H * W), quads, (__bf16*)out, nullptr, 0, -1);
-        else
-            hipLaunchKernelGGL((k_pack_input4<float, false>), dim3(g4), dim3(256), 0, to_stream(s), x, cin,
-                               (unsigned)(H * W), quads, (float*)out, nullptr, 0, -1);
-        return sd_check_launch("sd_pack_input");
-    }
     const int g = grid_for((long long)batch * H * W);
     if (dtype == SD_BF16)
         hipLaunchKernelGGL(k_pack_input<__bf16>, dim3(g), dim3(256), 0, to_stream(s), x, batch, cin, H, W, cpad,
@@ -376,18 +320,6 @@ extern "C" int sd_pack_input_amax(int dtype, const float* x, int batch, int cin,
     SD_REQUIRE(x && out && amax && batch > 0 && cin > 0 && H > 0 && W > 0 && slot >= 0 && clear != slot,
                "sd_pack_input_amax: bad args");
     SD_REQUIRE(cpad >= cin && cpad % 8 == 0, "sd_pack_input_amax: cpad %d", cpad);
-    if (pack4_ok(x, batch, cin, H, W, cpad)) {
-        const unsigned quads = (unsigned)((long long)batch * H * W / 4);
-        int g4 = grid_for(quads);
-        if (g4 > 512) g4 = 512;
-        if (dtype == SD_BF16)
-            hipLaunchKernelGGL((k_pack_input4<__bf16, true>), dim3(g4), dim3(256), 0, to_stream(s), x, cin,
-                               (unsigned)(H * W), quads, (__bf16*)out, amax, slot, clear);
-        else
-            hipLaunchKernelGGL((k_pack_input4<float, true>), dim3(g4), dim3(256), 0, to_stream(s), x, cin,
-                               (unsigned)(H * W), quads, (float*)out, amax, slot, clear);
-        return sd_check_launch("sd_pack_input_amax");
-    }
     int g = grid_for((long long)batch * H * W);
     if (g > 512) g = 512;  // grid-stride: at most 512 block maxima compete for the atomic
     if (dtype == SD_BF16)
