@@ -325,6 +325,26 @@ def infer_fp8(torch, model, dev, H=720, W=960, iters=20):
     return res
 
 
+def clock_probe(torch, L, dev, iters: int = 20000):
+    """Effective shader clock under MFMA load (sd_clock_probe: one block of 4 MFMA waves per CU, ~1 ms): MHz =
+    d(s_memtime) / d(s_memrealtime) x 100 per block, and the chip's back-to-back bf16 MFMA rate. Run right before and
+    right after the timed region, so box-to-box differences of the same binary can be told apart: a lower clock
+    (power/thermal state) moves both the probe and the kernels, contention or a slow memory system only the kernels."""
+    n = 256
+    if not hasattr(L.load(), "sd_clock_probe"):  # an older build of the C ABI (A/B runs)
+        return None
+    out = torch.zeros(4 * n, dtype=torch.int64, device=dev)
+    sink = torch.zeros(256, dtype=torch.float32, device=dev)
+    L.call("sd_clock_probe", n, iters, out.data_ptr(), sink.data_ptr(), L.stream_handle(dev))
+    torch.cuda.synchronize(dev)
+    o = out.view(n, 4).cpu().double()
+    mhz = ((o[:, 1] - o[:, 0]) / (o[:, 3] - o[:, 2]) * 100.0).sort().values
+    span_s = float(o[:, 3].max() - o[:, 2].min()) / 100e6
+    tflops = n * 4 * iters * 4 * 2 * 32 * 32 * 16 / span_s / 1e12
+    return {"mhz_median": round(float(mhz[n // 2]), 1), "mhz_min": round(float(mhz[0]), 1),
+            "mfma_tflops": round(tflops, 1), "probe_ms": round(span_s * 1e3, 3)}
+
+
 def cpu_baseline(seconds: float, height: int, width: int):
     """The oracle's fp32 PyTorch-CPU restatement of the reference train step (train.py:320-343)."""
     import torch
@@ -463,6 +483,7 @@ def main():
     torch.cuda.synchronize()
     log(f"warmup {args.warmup} steps: {time.perf_counter() - t_w:.1f}s")
 
+    clk_before = clock_probe(torch, L, dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -473,6 +494,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    clk_after = clock_probe(torch, L, dev)
 
     # Per-kernel HIP-event timing runs over a second K-step region right after the timed one: an
     # event record between two launches is a barrier packet on the stream (it serialises the queue
@@ -518,6 +540,9 @@ def main():
             "batchnorm": "sync" if (args.sync_bn and world > 1) else "per-rank",
         },
     }
+    result["clock"] = {"before": clk_before, "after": clk_after,
+                       "probe": "sd_clock_probe: 256 blocks x 4 waves of back-to-back bf16 MFMAs, ~1 ms, outside the "
+                                "timed region; MHz = d(s_memtime)/d(s_memrealtime) x 100"}
     if share:
         result["rehearsal"] = f"gloo, {world} ranks sharing cuda:0 (SD_BENCH_SHARE_DEVICE=1): not a scaling number"
     if world > 1:
@@ -562,6 +587,7 @@ def main():
             "launches_per_step": top["launches_per_step"],
             "region": f"HIP events around every conv/wgrad launch of {args.steps} steps after the timed region",
         }
+        result["clock"]["dominant_kernel"] = {"kernel": top["kernel"], "avg_launch_us": round(top["avg_us"], 2)}
         result["gemm_kernels"] = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()} for r in kern]
         result["encoder_conv_roofline"] = timer.encoder_roofline(args.steps, peak)
     if world == 1 and args.epe_steps > 0:

@@ -67,6 +67,10 @@ int sd_version(void);
 /* Diagnostics: device buffer for the per-wave cycle counters of timing builds (-DWG_EXP=1024; no effect
    otherwise). Not a reference interface. */
 int sd_debug_buffer(void* dev_ptr);
+/* Diagnostics: effective shader clock under MFMA load (bench.py "clock"). blocks x 256 threads of back-to-back bf16
+   MFMAs; out[4 * block + {0,1,2,3}] = s_memtime start/end, s_memrealtime (100 MHz) start/end; sink: >= 256 floats
+   (never written in practice). Not a reference interface. */
+int sd_clock_probe(int blocks, int iters, unsigned long long* out, float* sink, sd_stream s);
 const char* sd_last_error(void);
 int sd_device_init(int device);
 

@@ -108,6 +108,7 @@ _WJOB = ctypes.POINTER(SdWredJob)
 PROTOTYPES: dict[str, tuple] = {
     "sd_version": (_i, []),
     "sd_debug_buffer": (_i, [_p]),
+    "sd_clock_probe": (_i, [_i, _i, _p, _p, _p]),
     "sd_last_error": (ctypes.c_char_p, []),
     "sd_device_init": (_i, [_i]),
     "sd_pack_input": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _p]),

@@ -235,6 +235,10 @@ struct HFwdArgs {
 #ifndef HC_ST_AUX
 #define HC_ST_AUX 2
 #endif
+// weight images by LDS-DMA in the multi-chunk M16 conv instances (k_halo_conv loaders); HC_WDMA=0 builds: register-staged
+#ifndef HC_WDMA
+#define HC_WDMA 1
+#endif
 // the vertical-reuse k-loop of the N = 32 RT = 4 conv instances (k_halo_conv); HC_VR=0 builds: the per-tap loop
 #ifndef HC_VR
 #define HC_VR 1
@@ -311,26 +315,12 @@ __device__ __forceinline__ int ld_piece(int item) { return (item >> 3) % PPX; }
 // keeps bf16's relative precision on the normalised activation: where a channel's |mean| / std is large (enc1.0: ~4.6
 // on a trained checkpoint) the rounding of y, magnified by scale, was the largest activation error of the bf16 path
 // (tools/precision_study.py: per-batch EPE noise 1.5e-3 -> 5.4e-4 px, as much as fp32 storage would give).
-// WRJ (1 or 2: weights in registers, training forwards and dgrads of the N % 64 layers whose width tiles by 16 or 32):
-// the loaders stage only the halo; each MFMA wave owns 16 of the block's 64 output channels over the whole 256-pixel
-// tile (16 x 16 or 8 x 32: WRJ 16-pixel column sets per row) and reads its A fragments (the chunk's 9 taps x 16 rows
-// x 32 channels) straight from the packed weights in L2 into registers, one chunk ahead. Per chunk and CU that removes
-// the 36 KB weight staging writes and the A-fragment reads from the LDS, which the fragment reads and staging writes
-// of the LDS-weight form kept ~84 % busy; the halo fragments are read once per (halo row, kw) and feed the three
-// output rows hr - kh (vertical reuse, taps in the order 0..8 per output row, so the sums are the LDS-weight M16
-// instance's bit for bit). Results leave through a block-wide scratch (all 64 channels of a pixel in one 128-B row,
-// read back after the next barrier), so the stores stay whole-line.
-// Measured (r04, tools/conv_micro.py, same box): 5-28 % SLOWER than the LDS-weight instances at every N % 64 shape
-// of the model, so it is opt-in (SD_HALO_WR=1, halo_wr_cols). The per-chunk weight reloads wait behind the loader
-// waves' HBM-missing halo loads (a timing build without reloads was 15-20 % faster on the multi-chunk layers; loading
-// two chunks ahead spills), and the LDS-weight form was not bound by the LDS bandwidth it saves: its one- and
-// two-chunk layers keep their weights in LDS for the whole launch (WCONST) and still beat this form's no-reload bound.
-// (the body of both kernels below: k_halo_conv keeps its rocprofv3 names, k_halo_conv_wr is the WRJ form)
-template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF, int WRJ>
+// (Weights in registers for the N % 64 layers, each MFMA wave owning 16 output channels over a whole 256-pixel tile
+// with its A fragments read from L2 one chunk ahead, was built in r04 and measured 5-28 % slower than these LDS-weight
+// instances at every N % 64 shape: DESIGN.md §3 r04. Removed in r05.)
+template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF>
 __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
     static_assert(!(OAFF && (STATS || BNS)), "the affine epilogue stores eval-mode outputs (no statistics)");
-    constexpr bool NOW = WRJ > 0;  // no weights in the LDS
-    static_assert(!NOW || (NT == 2 && CK == 32 && IT == 1 && !BNS && !OAFF && !WCONST), "WRJ: 64-channel training blocks");
     constexpr int BN = 32 * NT;
     constexpr int PPX = CK / 8;                          // 16-B pieces per pixel (and per tap of a weight row)
     // M16 (every CK = 32 instance but the BNS dgrads): v_mfma_f32_16x16x32_bf16, one k-step per tap. Same LDS bytes and
@@ -350,22 +340,20 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
     // spills 75-122 VGPRs in this form: its y pieces, BatchNorm constants and sums sit beside the accumulators.)
     constexpr bool M16 = CK == 32 && IT == 1 && !BNS;
     constexpr int HX_LD = halo_ld(CK), W_LD = M16 ? 9 * CK : wrow_ld(CK);
-    // IT = 2: the CK = 32 tilings (halo <= 384 px); WRJ: 10 x 34 or 18 x 18 halos
-    constexpr int HPX = IT == 2 || NOW ? 384 : halo_px_cap(RT, CK);
+    // IT = 2: the CK = 32 tilings (halo <= 384 px)
+    constexpr int HPX = IT == 2 ? 384 : halo_px_cap(RT, CK);
     constexpr int HP = (HPX * PPX + 255) / 256;          // halo pieces per loader thread
     constexpr int WPIECES = BN * 9 * PPX;                // weight pieces per chunk
     constexpr int W_PER_THREAD = (WPIECES + 255) / 256;
     static_assert(!M16 || (HP * 256 == HPX * PPX && HPX % 16 == 0), "M16: the loader pieces tile the halo exactly");
     constexpr int HALO_ITEM = M16 ? HPX * CK : HP * 256 / PPX * HX_LD;  // one item's halo region
-    constexpr int HALO_ELEMS = IT * HALO_ITEM, W_ELEMS = NOW ? 0 : BN * W_LD, BUF = HALO_ELEMS + W_ELEMS;
+    constexpr int HALO_ELEMS = IT * HALO_ITEM, W_ELEMS = BN * W_LD, BUF = HALO_ELEMS + W_ELEMS;
     static_assert(IT == 1 || (IT == 2 && HP * IT <= 16), "item masks fit 16 bits");
     constexpr int KS = (9 * CK + 15) / 16;               // 16-deep k-steps per chunk (CK 8: 5, the last half padding)
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
     // epilogue transpose scratch: 32 (M16: 16) pixels x BN channels per MFMA wave (its own region, no block sync)
     constexpr int SCR_PX = M16 ? 16 : 32;
-    __shared__ __attribute__((aligned(16))) __bf16 scr[NOW ? 8 : 4 * SCR_PX * BN];
-    // WRJ: the block's results of an item, [pixel][64 channels] (16-B pieces XOR-swizzled by pixel), two items deep
-    __shared__ __attribute__((aligned(16))) __bf16 escr[NOW ? 2 * 256 * BN : 8];
+    __shared__ __attribute__((aligned(16))) __bf16 scr[4 * SCR_PX * BN];
 
     // waves 0-3 land on the 4 different SIMDs (dispatch order 0->2->1->3, measured), and so do 4-7:
     // one MFMA wave and one loader wave per SIMD
@@ -476,6 +464,7 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
         // weights: byte offset of each piece in chunk 0 (OOB: past the weight rows of this N-block)
         const __amdgpu_buffer_rsrc_t wrs =
             __builtin_amdgcn_make_buffer_rsrc((void*)p.wp, (short)0, p.N * p.kpad * 2, 0x00020000);
+        constexpr bool WDMA = HC_WDMA && M16 && !WCONST && IT == 1;  // weights by LDS-DMA (below)
         unsigned woff[W_PER_THREAD];
 #pragma unroll
         for (int i = 0; i < W_PER_THREAD; ++i) {
@@ -483,8 +472,34 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
             const int co = item / (9 * PPX), r = item - co * (9 * PPX), tap = r / PPX, sp = r - tap * PPX;
             woff[i] = ((item < WPIECES) & (n0 + co < p.N)) ? (unsigned)((n0 + co) * p.kpad + tap * wct + sp * 8) * 2u
                                                           : OOB;
-            asm volatile("" : "+v"(woff[i]));  // kept in registers, not recomputed per chunk
+            if constexpr (!WDMA) asm volatile("" : "+v"(woff[i]));  // kept in registers, not recomputed per chunk
         }
+        // WDMA (the multi-chunk M16 instances): the chunk's weight image goes global -> LDS by LDS-DMA
+        // (buffer_load_dwordx4 ... lds: no VGPR destination, no ds_write). The M16 weight image is BN unpadded rows of
+        // 36 16-B slots, contiguous, so wave-instruction k of a chunk fills LDS slots 64k .. 64k + 63 (M0 + 16 * lane)
+        // and each lane's SOURCE address carries the row's piece swap: slot s = 36 co + rs holds piece rs ^ wswz(co).
+        // The DMA of chunk g is issued in loader iteration g after the halo stores, into buffer g & 1 (free since the
+        // barrier that ended iteration g - 1), and waited for by a counted vmcnt (the halo loads issued after it may
+        // stay in flight) before the iteration's barrier. hipcc does not see the asm loads, so its own counted waits
+        // only grow stricter: each one also covers a DMA that the previous iteration's vmcnt already retired.
+        // This replaces 9 buffer_load_dwordx4 + 9 ds_write_b128 per loader thread and chunk: the VGPR -> LDS transfer
+        // of the stores (13 cycles each) was what the loader waves waited on (SQ_WAIT_INST_LDS).
+        constexpr int NWI = WPIECES / 64;                   // wave-instructions per chunk
+        constexpr int WDI = WDMA ? (NWI + 3) / 4 : 1;       // per loader wave
+        static_assert(!WDMA || (WPIECES % 64 == 0 && (HALO_ELEMS * 2) % 16 == 0 && (BUF * 2) % 16 == 0), "WDMA image");
+        const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+        unsigned wdoff[WDI];
+        if constexpr (WDMA) {
+#pragma unroll
+            for (int j = 0; j < WDI; ++j) {
+                const int k = wid_u * WDI + j, s = k * 64 + lane;
+                const int co = s / (9 * PPX), rs = s - co * (9 * PPX), r = rs ^ wswz(co);
+                const int tap = r / PPX, sp = r - tap * PPX;
+                wdoff[j] = (k < NWI && n0 + co < p.N) ? (unsigned)((n0 + co) * p.kpad + tap * wct + sp * 8) * 2u : OOB;
+                asm volatile("" : "+v"(wdoff[j]));
+            }
+        }
+        const unsigned lds_w0 = (unsigned)(uintptr_t)(smem + HALO_ELEMS) + (unsigned)(wid_u * WDI) * 1024u;
         // Software pipeline, one iteration per chunk g: store chunk g (set g % LS, loaded LS iterations ago) and
         // the weights of chunk g (loaded one iteration ago) into LDS buffer g & 1, load the weights of chunk g+1
         // and the halo of chunk g+LS, barrier; the MFMA waves compute chunk g-1 meanwhile. Every iteration
@@ -544,6 +559,33 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
             }
         };
         auto load_w = [&]() __attribute__((always_inline)) { load_w_into(wr); };
+        // WDMA: chunk w_cc's weight image -> LDS buffer buf (this wave's WDI KiB of it), advance. No per-piece masks of
+        // a partial chunk: its pieces past the source's channels read other (finite) weights of the layer, which meet
+        // the zero halo pieces of those channels.
+        auto dma_w = [&](int buf) __attribute__((always_inline)) {
+            const int wv = c_lo + w_cc;
+            const bool lo = wv >= ncp;
+            const int wc = lo ? wv - ncp : wv;
+            const bool s1 = wc >= nc0;
+            const int cl = (s1 ? wc - nc0 : wc) * CK;
+            if (++w_cc == nchunks) w_cc = 0;
+            const unsigned soff = __builtin_amdgcn_readfirstlane(((s1 ? p.a.c0 : 0) + cl + (lo ? p.a.ctot : 0)) * 2);
+            const unsigned m0b = __builtin_amdgcn_readfirstlane(lds_w0 + (unsigned)(buf * BUF * 2));
+#pragma unroll
+            for (int j = 0; j < WDI; ++j) {
+                if (NWI % 4 != 0 && wid_u * WDI + j >= NWI) break;  // wave-uniform
+                unsigned keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\t"
+                    "s_mov_b32 m0, %2\n\t"
+                    "s_nop 0\n\t"
+                    "buffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+                    "s_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "v"(wdoff[j]), "s"(m0b + (unsigned)j * 1024u), "s"(wrs), "s"(soff)
+                    : "memory");
+            }
+        };
         auto store_w_from = [&](int buf, const uint4 (&wsrc)[W_PER_THREAD]) __attribute__((always_inline)) {
             __bf16* wl = smem + buf * BUF + HALO_ELEMS;
 #pragma unroll
@@ -621,7 +663,7 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
                                      : ld_pixel<PPX>(item) * HX_LD + ld_piece<PPX>(item) * 8;
                 *reinterpret_cast<uint4*>(hx + u * HALO_ITEM + hoff) = v;
             }
-            if constexpr (!WCONST && !NOW) if (!(WG_EXP & 131072)) store_w(buf);
+            if constexpr (!WCONST && !WDMA) if (!(WG_EXP & 131072)) store_w(buf);
         };
         constexpr std::integral_constant<int, 0> S0{};
         constexpr std::integral_constant<int, 1> S1{};
@@ -643,9 +685,19 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
             if (DG) t0 = __builtin_amdgcn_s_memtime();
             if (!(WG_EXP & 65536)) store(U, decltype(U)::value & 1);
             stamp(t_st);
-            if constexpr (!WCONST && !NOW) if (!(WG_EXP & 65536)) load_w();
+            if constexpr (WDMA) {
+                __builtin_amdgcn_sched_barrier(0);
+                dma_w(decltype(U)::value & 1);
+                __builtin_amdgcn_sched_barrier(0);
+            } else if constexpr (!WCONST) {
+                if (!(WG_EXP & 65536)) load_w();
+            }
             if (!(WG_EXP & 65536)) load(U);
             stamp(t_ld);
+            if constexpr (WDMA) {  // this chunk's weight DMA landed; the halo loads just issued stay in flight
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"i"(IT * HP) : "memory");
+            }
             __syncthreads();
             stamp(t_br);
         };
@@ -670,7 +722,7 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
                 load(S2);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if constexpr (!WCONST && !NOW) load_w();
+            if constexpr (!WCONST && !WDMA) load_w();
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (LS == 4) load(S3);
             else load(S1);
@@ -702,7 +754,6 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
             d[2] = t_br;
             d[3] = __builtin_amdgcn_s_memtime() - t_all;
         }
-        if constexpr (NOW) __syncthreads();  // WRJ: the last item's scratch (MFMA waves)
         __syncthreads();  // stats reduction barrier (MFMA waves)
         return;
     }
@@ -721,188 +772,6 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
 #pragma unroll
     for (int j = 0; j < NOWN; ++j) own[j] = 0.f;
     constexpr int PPP = NT * 4;      // 16-B pieces per pixel row
-    if constexpr (NOW) {
-        // ----------------------------------------------------------- WRJ: weights in registers (see the template)
-        constexpr int J = WRJ, TH = 16 / J, TW = 16 * J;      // tile rows and width (p.th, p.tw: host REQUIRE)
-        constexpr int NH = TH + 2, HWV = TW + 2, NS = 3 * NH;  // halo rows and width, steps (halo row, kw)
-        constexpr int PV = 2;                                  // halo fragment read-ahead (steps; 4 measured no faster)
-        constexpr unsigned OOBW = 0x80000000u;
-        const __amdgpu_buffer_rsrc_t wrs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)p.wp, (short)0, p.N * p.kpad * 2, 0x00020000);
-        // A fragment (16x16x32): lane l holds output channel n0 + 16*wid + (l & 15), channels 8*(l >> 4) + 0..7 of the
-        // chunk at each tap; 16 rows x 64 B per load
-        const int co = n0 + 16 * wid + (lane & 15);
-        const unsigned wlb = co < p.N ? (unsigned)(co * p.kpad + 8 * (lane >> 4)) * 2u : OOBW;
-        bf16x8 aw[9], an[9];  // this chunk's taps, the next chunk's (in flight)
-        f32x4 accw[16];       // 16-pixel blocks (tile pixels 16 i .. 16 i + 15) x this wave's 16 channels
-        auto load_chunk = [&](int cv, auto& an) __attribute__((always_inline)) {  // chunk cv of an item -> an
-            const int wv = c_lo + cv;
-            const bool lo = wv >= ncp;  // wsplit: the second pass reads the lo halves
-            const int wc = lo ? wv - ncp : wv;
-            const bool s1 = wc >= nc0;
-            const int C = s1 ? p.a.c1 : p.a.c0;
-            const int cl = (s1 ? wc - nc0 : wc) * CK;
-            const int kb = (s1 ? p.a.c0 : 0) + cl + (lo ? p.a.ctot : 0);
-            const unsigned vo = cl + 8 * (lane >> 4) < C ? wlb : OOBW;  // pieces past the source's channels: zeros
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap)
-                an[tap] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, vo, (tap * wct + kb) * 2, 0));
-        };
-        // item end: lane l holds channels 4 (l >> 4) + 0..3 of pixel l & 15 of each 16-pixel block; v_permlane16_swap
-        // on blocks (2g, 2g + 1) gives lane l the whole 8-channel piece (l >> 5) of pixel l & 15 of block
-        // 2g + ((l >> 4) & 1), written to the scratch row of that pixel
-        auto epi_write = [&](int par) __attribute__((always_inline)) {
-            __bf16* const e = escr + par * 256 * BN;
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                unsigned pw[2][2];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    bf16x4 v;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = (__bf16)accw[2 * g + h][q];
-                    const uint2 u = __builtin_bit_cast(uint2, v);
-                    pw[h][0] = u.x;
-                    pw[h][1] = u.y;
-                }
-                const auto rx = __builtin_amdgcn_permlane16_swap(pw[0][0], pw[1][0], false, false);
-                const auto ry = __builtin_amdgcn_permlane16_swap(pw[0][1], pw[1][1], false, false);
-                const int px = 32 * g + 16 * ((lane >> 4) & 1) + (lane & 15);
-                const int cp = 2 * wid + (lane >> 5);  // 8-channel piece of the 64-channel row
-                *reinterpret_cast<uint4*>(e + px * BN + ((cp ^ (px & 7)) * 8)) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-            }
-        };
-        // after the next barrier: wave w stores tile pixels 64 w .. 64 w + 63, 8 pixels x 8 pieces per instruction
-        auto epi_read_t = [&](int par, int item, auto SPL) __attribute__((always_inline)) {
-            const __bf16* const e = escr + par * 256 * BN;
-            const int sp = slot + item * p.gper;
-            const int b = sp / p.tiles, tl = sp - b * p.tiles;
-            const int ty = tl / p.tiles_x;
-            const int h0 = ty * TH, w0 = (tl - ty * p.tiles_x) * TW;
-            const int hw_img = p.H * p.W;
-            constexpr bool split = decltype(SPL)::v;
-            const int ns = split ? p.n_split : p.N;
-            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(p.out0 + (size_t)b * hw_img * ns), (short)0, hw_img * ns * 2, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(split ? p.out1 + (size_t)b * hw_img * (p.N - ns) : p.out0), (short)0,
-                split ? hw_img * (p.N - ns) * 2 : 0, 0x00020000);
-            const int j = lane & 7, c = n0 + 8 * j;
-            uint4 v[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int px = 64 * wid + 8 * r + (lane >> 3);
-                v[r] = *reinterpret_cast<const uint4*>(e + px * BN + ((j ^ (px & 7)) * 8));
-            }
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int px = 64 * wid + 8 * r + (lane >> 3);
-                const int h = h0 + px / TW, w = w0 + px % TW;
-                const bool live = (h < p.H) & (w < p.W);
-                if constexpr (STATS) stats_add(own, v[r], live);
-                __attribute__((ext_vector_type(4))) unsigned data = {v[r].x, v[r].y, v[r].z, v[r].w};
-                const int pix = h * p.W + w;
-                if constexpr (!split) {
-                    const unsigned off = (live & (c < p.N)) ? (unsigned)(pix * p.N + c) * 2u : OOBW;
-                    __builtin_amdgcn_raw_buffer_store_b128(data, rs0, off, 0, 0);
-                } else {  // dgrad of a concatenation: channels < n_split to out0, the rest to out1
-                    const unsigned o0 = (live & (c < ns)) ? (unsigned)(pix * ns + c) * 2u : OOBW;
-                    const unsigned o1 = (live & (c >= ns) & (c < p.N)) ? (unsigned)(pix * (p.N - ns) + c - ns) * 2u : OOBW;
-                    __builtin_amdgcn_raw_buffer_store_b128(data, rs0, o0, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(data, rs1, o1, 0, 0);
-                }
-            }
-        };
-        const bool split_out = p.epi == SD_EPI_SPLIT || p.epi == SD_EPI_SPLIT_STATS;
-        auto epi_read = [&](int par, int item) __attribute__((always_inline)) {
-            if (split_out) epi_read_t(par, item, BoolC<true>{});
-            else epi_read_t(par, item, BoolC<false>{});
-        };
-        constexpr bool DGW = (WG_EXP & 1024) != 0;
-        unsigned long long w_cp = 0, w_ep = 0, w_br = 0, w0 = 0, w_all = DGW ? __builtin_amdgcn_s_memtime() : 0;
-        load_chunk(0, an);
-        int cc = 0, pass = 0, pend = -1;
-        for (int gi = 0; gi < total; ++gi) {
-            if (DGW) w0 = __builtin_amdgcn_s_memtime();
-            __syncthreads();  // chunk gi is in buffer gi & 1; the scratch of the item that ended with chunk gi - 1 is whole
-            if (DGW) {
-                const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-                w_br += t1 - w0;
-                w0 = t1;
-            }
-            // this chunk's weights (loaded a chunk ago) before anything else is issued: the wait for them must not
-            // also wait for the scratch read-back's stores (VMEM operations complete in order)
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) aw[tap] = an[tap];
-            __builtin_amdgcn_sched_barrier(0);
-            load_chunk(cc + 1 == nchunks ? 0 : cc + 1, an);
-            if (cc == 0) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) accw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            // halo fragment of (halo row hr, column set jj, kw): lane l reads piece l >> 4 of halo pixel
-            // (hr, 16 jj + kw + (l & 15)) of the piece-major halo; steps run (hr, kw) so every output row meets its taps
-            // in the order 0..8
-            const __bf16* const xb = smem + (gi & 1) * BUF + (lane >> 4) * HPX * 8 + (lane & 15) * 8;
-            bf16x8 xv[PV + 1][J];
-            auto readX = [&](int st) __attribute__((always_inline)) {
-                const int hr = st / 3, kw = st % 3;
-#pragma unroll
-                for (int jj = 0; jj < J; ++jj)
-                    xv[st % (PV + 1)][jj] = *reinterpret_cast<const bf16x8*>(xb + (hr * HWV + 16 * jj + kw) * 8);
-            };
-#pragma unroll
-            for (int st = 0; st < PV; ++st) readX(st);
-#pragma unroll
-            for (int st = 0; st < NS; ++st) {
-                const int hr = st / 3, kw = st % 3;
-                if (st + PV < NS) readX(st + PV);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int kh = 0; kh < 3; ++kh) {
-                    const int s = hr - kh;  // output row of this (halo row, kernel row) pair
-                    if (s < 0 || s >= TH) continue;
-#pragma unroll
-                    for (int jj = 0; jj < J; ++jj)
-                        accw[s * J + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[kh * 3 + kw], xv[st % (PV + 1)][jj],
-                                                                                 accw[s * J + jj], 0, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                // the previous item's read-back and stores behind the chunk's last MFMAs (in flight meanwhile; after
-                // the second halo row instead: 6 % slower, the branch costs the LDS-read waits that follow it)
-                if (st == NS - 1 && pend >= 0) {
-                    epi_read(pend & 1, pend);
-                    pend = -1;
-                }
-            }
-            if (DGW) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-                w_cp += t1 - w0;
-                w0 = t1;
-            }
-            if (++cc == nchunks) {
-                epi_write(pass & 1);
-                pend = pass;
-                cc = 0;
-                ++pass;
-                if (DGW) {
-                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                    w_ep += __builtin_amdgcn_s_memtime() - w0;
-                }
-            }
-        }
-        if (DGW && p.dbg && lane == 0) {
-            unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + wid) * 4;
-            d[0] = w_cp;
-            d[1] = w_ep;
-            d[2] = w_br;
-            d[3] = __builtin_amdgcn_s_memtime() - w_all;
-        }
-        for (int e = total; e < padded; ++e) __syncthreads();  // the loaders' iterations past the last chunk
-        __syncthreads();  // the last item's scratch
-        if (pend >= 0) epi_read(pend & 1, pend);
-    } else {
     // 32-pixel column tile i of this MFMA wave: the M16 instances own RT consecutive ones (in 32-pixel-wide tiles, RT
     // consecutive rows: what the vertical-reuse k-loop below needs), the others every fourth
     // The N = 32 RT = 4 BNS dgrads (32x32x16 MFMAs, VR32) run the same vertical reuse on 32-pixel fragments (one tile row
@@ -1469,7 +1338,6 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
         d[2] = t_br;
         d[3] = __builtin_amdgcn_s_memtime() - t_all;
     }
-    }  // !NOW
 
     // ---------------------------------------------------------------- BN statistics row
     if constexpr (STATS || BNS) {
@@ -1500,11 +1368,7 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
 
 template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF = false>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
-    halo_conv_body<NT, RT, CK, STATS, WCONST, IT, BNS, OAFF, 0>(p);
-}
-template <bool STATS, int WRJ>
-__global__ __launch_bounds__(512) void k_halo_conv_wr(const HFwdArgs p) {
-    halo_conv_body<2, 2, 32, STATS, false, 1, false, false, WRJ>(p);
+    halo_conv_body<NT, RT, CK, STATS, WCONST, IT, BNS, OAFF>(p);
 }
 
 // =====================================================================================
@@ -2219,19 +2083,7 @@ static int halo_prio(const sd_src& a) {
 struct HTile {
     int th, tw, rt, ck;
     int it = 1;  // items per pass (k_halo_conv IT)
-    int wr = 0;  // k_halo_conv WRJ (weights in registers): 16-pixel column sets per tile row
 };
-// the weights-in-registers instances (k_halo_conv WRJ) for the training launches of the N % 64 layers whose width
-// tiles by 32 (8 x 32 tiles) or 16 (16 x 16): SD_HALO_WR=1 (read per call). Off by default: measured 5-28 % slower
-// than the LDS-weight instances over the model's N % 64 shapes (tools/conv_micro.py --modes=default,wr1, DESIGN.md
-// r04), the weight reloads from L2 wait behind the loaders' HBM misses, and without reloads (a timing-only build)
-// it was ahead on two layers by 3-5 % only
-static int halo_wr_cols(int W, int N, bool wr_ok) {
-    if (!wr_ok || N % 64 != 0) return 0;
-    const char* e = getenv("SD_HALO_WR");
-    if (!(e && atoi(e) == 1)) return 0;
-    return W % 32 == 0 ? 2 : (W % 16 == 0 ? 1 : 0);
-}
 // per-CU cycles of one chunk: the MFMA pipe of one SIMD vs the LDS (fragment reads at 4 cycles per
 // ds_read_b128, staging stores at ~79 B/cycle: MI355X_MICROARCH.md LDS table)
 static double halo_chunk_cycles(int th, int tw, int rt, int ck, int nt) {
@@ -2241,13 +2093,8 @@ static double halo_chunk_cycles(int th, int tw, int rt, int ck, int nt) {
     const double stores = ((double)(th + 2) * (tw + 2) * ck * 2 + 32.0 * nt * 9 * ck * 2) / 79.0;
     return mfma > reads + stores ? mfma : reads + stores;
 }
-static HTile halo_tile(int H, int W, int N, bool stats, bool wr_ok) {
+static HTile halo_tile(int H, int W, int N, bool stats) {
     const int nt = N == 32 ? 1 : 2;
-    if (const int j = halo_wr_cols(W, N, wr_ok)) {
-        HTile t{16 / j, 16 * j, 2, 32};
-        t.wr = j;
-        return t;
-    }
     // CK = 32 (RT <= 3) measured faster than the CK = 16 / 512-pixel tiling at every N % 64 layer of
     // the 320x240 step (tools/conv_micro.py); SD_HALO_CK=16 selects the latter (tests, experiments)
     const char* env = getenv("SD_HALO_CK");
@@ -2313,7 +2160,7 @@ static void halo_grid(const HTile& t, int batch, int H, int W, int N, int& nblk,
 // stats rows of the forward (STATS) launch
 int sd_halo_fwd_rows(int batch, int H, int W, int N) {
     int nblk, gper, nsp;
-    halo_grid(halo_tile(H, W, N, true, true), batch, H, W, N, nblk, gper, nsp);
+    halo_grid(halo_tile(H, W, N, true), batch, H, W, N, nblk, gper, nsp);
     return gper;
 }
 
@@ -2328,10 +2175,10 @@ static int halo_it_env() {
     }();
     return v;
 }
-static HTile fwd_tile(int ctot, int H, int W, int N, bool stats, bool wr_ok) {
-    HTile t = halo_tile(H, W, N, stats, wr_ok);
+static HTile fwd_tile(int ctot, int H, int W, int N, bool stats) {
+    HTile t = halo_tile(H, W, N, stats);
     if (ctot <= 8 && N == 32) t.ck = 8;
-    if (t.wr == 0 && halo_it_env() == 2 && N % 64 == 0 && t.ck == 32 && ctot > 32 && t.rt == 2 &&
+    if (halo_it_env() == 2 && N % 64 == 0 && t.ck == 32 && ctot > 32 && t.rt == 2 &&
         (t.th + 2) * (t.tw + 2) <= 384) {
         t.ck = 16;
         t.it = 2;
@@ -2342,12 +2189,12 @@ static HTile fwd_tile(int ctot, int H, int W, int N, bool stats, bool wr_ok) {
 // partial rows of a STORE launch (sd_conv_gemm_bnsum): one per block of an N-block, like STATS
 int sd_halo_store_rows(int batch, int H, int W, int N, int ctot) {
     int nblk, gper, nsp;
-    halo_grid(fwd_tile(ctot, H, W, N, false, false), batch, H, W, N, nblk, gper, nsp);  // BNS launches
+    halo_grid(fwd_tile(ctot, H, W, N, false), batch, H, W, N, nblk, gper, nsp);  // BNS launches
     return gper;
 }
 bool sd_halo_bnsum_ok(const sd_src& a, int N) {
     if (!sd_halo_fwd_ok(a, N, SD_EPI_STORE)) return false;
-    const HTile t = fwd_tile(a.chans[0] + a.chans[1], a.H, a.W, N, false, false);
+    const HTile t = fwd_tile(a.chans[0] + a.chans[1], a.H, a.W, N, false);
     return t.ck == 32 && t.it == 1 && !(N != 32 && t.rt == 3);
 }
 
@@ -2365,11 +2212,7 @@ static bool wconst_chunks(int nchunks) {
 const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns, bool wsplit, bool oaff) {
     static thread_local char buf[64];
     const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
-    const HTile t = fwd_tile(c0 + c1, H, W, N, stats, !bns && !oaff);
-    if (t.wr) {
-        snprintf(buf, sizeof(buf), "k_halo_conv_wr<%s, %d>", stats ? "true" : "false", t.wr);
-        return buf;
-    }
+    const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
     const bool wc = wconst_chunks((cdiv(c0, t.ck) + cdiv(c1, t.ck)) * (wsplit ? 2 : 1));
     const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
     if (oaff)
@@ -2485,7 +2328,7 @@ static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, cons
 
 // split-K workspace bytes of an eval STORE launch (0: the shape runs unsplit)
 long long sd_halo_split_ws_bytes(const sd_src& a, int batch, int H, int W, int N, int epi, bool wsplit) {
-    const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, false, false);  // eval launches
+    const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, false);  // eval launches
     int nblk, gper, nsp;
     halo_grid(t, batch, H, W, N, nblk, gper, nsp);
     const int nch = cdiv(a.chans[0], t.ck) + cdiv(a.chans[1], t.ck);
@@ -2497,7 +2340,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
                      void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns, bool wsplit,
                      const float* osc, const float* osh, void* ws, long long ws_bytes) {
     const bool st_ = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
-    const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_, !osc && !bns);
+    const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_);
     HFwdArgs p;
     p.a = make_halo_src(a);
     p.H = H;
@@ -2536,7 +2379,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
         p.bis = bns->invstd;
     }
     const int nch = cdiv(p.a.c0, t.ck) + cdiv(p.a.c1, t.ck);
-    HSplit q = halo_split_plan(t, p.nblk, p.gper, p.nsp, N, nch * (wsplit ? 2 : 1), epi, bns != nullptr || t.wr);
+    HSplit q = halo_split_plan(t, p.nblk, p.gper, p.nsp, N, nch * (wsplit ? 2 : 1), epi, bns != nullptr);
     const long long need = q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
     if (q.ksplit > 1 && (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0)) {  // no workspace: one group
         q.ksplit = 1;
@@ -2566,16 +2409,7 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     SD_REQUIRE(!(N == 32 && t.ck == 32 && t.rt == 4) || (t.th == 16 && t.tw == 32),
                "sd_conv_gemm(halo): the N = 32 RT 4 instances (vertical reuse) need 16x32 tiles, got %dx%d", t.th, t.tw);
     SD_REQUIRE(t.ck != 8 || nch == 1, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
-    SD_REQUIRE(!t.wr || (N % 64 == 0 && t.ck == 32 && t.it == 1 && t.tw == 16 * t.wr && t.th * t.tw == 256 &&
-                         !q.nt1 && q.ksplit == 1 && !osc && !bns && p.nhalo <= 384),
-               "sd_conv_gemm(halo): weights-in-registers tile %dx%d", t.th, t.tw);
-    if (t.wr == 2) {
-        if (st_) hipLaunchKernelGGL((k_halo_conv_wr<true, 2>), grid, dim3(512), 0, st, p);
-        else hipLaunchKernelGGL((k_halo_conv_wr<false, 2>), grid, dim3(512), 0, st, p);
-    } else if (t.wr == 1) {
-        if (st_) hipLaunchKernelGGL((k_halo_conv_wr<true, 1>), grid, dim3(512), 0, st, p);
-        else hipLaunchKernelGGL((k_halo_conv_wr<false, 1>), grid, dim3(512), 0, st, p);
-    } else if (q.nt1) {  // 32-channel N-blocks of an N % 64 layer (batch-1 eval)
+    if (q.nt1) {  // 32-channel N-blocks of an N % 64 layer (batch-1 eval)
         if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p);
         else launch_halo<1, 2, 32>(st_, wc, grid, st, p);
     } else if (t.ck == 8) {

@@ -30,6 +30,47 @@ extern "C" int sd_device_init(int device) {
     return SD_OK;
 }
 
+// Effective shader clock under MFMA load (bench.py "clock"): every block runs 4 waves of back-to-back
+// v_mfma_f32_32x32x16_bf16 (4 independent accumulator chains per wave) and wave 0 stamps the shader-clock counter
+// (s_memtime) and the 100 MHz constant clock (s_memrealtime) around its loop: clock = d(memtime) / d(realtime) * 100
+// MHz. One block per CU loads the whole chip the way the persistent conv kernels do. out[4 * block + {0..3}] = (memtime
+// start, memtime end, realtime start, realtime end).
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void k_clock_probe(int iters, unsigned long long* __restrict__ out,
+                                                     float* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    bf16x8 a, b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // random-looking operands (the power draw of real data, not of zeros)
+        a[i] = (__bf16)(((lane * 37 + i * 11) % 17) * 0.0625f - 0.5f);
+        b[i] = (__bf16)(((lane * 13 + i * 7) % 19) * 0.0625f - 0.55f);
+    }
+    f32x16_t acc[4] = {};
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[c], 0, 0, 0);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s += acc[c][0] + acc[c][15];
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (s == 12345.f) sink[threadIdx.x] = s;  // keeps the chains live
+    if (threadIdx.x == 0) {
+        out[4 * blockIdx.x] = t0;
+        out[4 * blockIdx.x + 1] = t1;
+        out[4 * blockIdx.x + 2] = r0;
+        out[4 * blockIdx.x + 3] = r1;
+    }
+}
+
+extern "C" int sd_clock_probe(int blocks, int iters, unsigned long long* out, float* sink, sd_stream s) {
+    SD_REQUIRE(blocks > 0 && iters > 0 && out && sink, "sd_clock_probe: bad args");
+    hipLaunchKernelGGL(k_clock_probe, dim3(blocks), dim3(256), 0, to_stream(s), iters, out, sink);
+    return sd_check_launch("sd_clock_probe");
+}
+
 namespace {
 
 // ------------------------------------------------------------------ packing

@@ -117,6 +117,7 @@ class UNetEngine:
         self._amax_host: torch.Tensor | None = None  # pinned copies
         self._amax_ev: list = [None, None, None]
         self._amax_used: list = [False, False, False]
+        self._amax_checked: list = [True, True, True]  # whether _fp8_policy has compared that word's read-back
         self._amax_packed = None
         self._amax_pending: int | None = None
         self._fp8_cal = None  # (slot, event) of the calibration frame's amax
@@ -172,6 +173,9 @@ class UNetEngine:
         # storage of y would give); consumers then apply only the ReLU. SD_ZSTORE=0: store y.
         self.zstore = precision == "bf16" and os.environ.get("SD_ZSTORE", "1") != "0"
         self._zs: set = set()
+        # the current forward may be backpropagated (forward(need_backward=True): an eval-mode forward through
+        # autograd, e.g. frozen-BatchNorm fine-tuning): no BN-applied stores then, since the backward reads the raw y
+        self._zs_ok = True
         self._one = torch.ones(16 * base_channels, dtype=torch.float32, device=self.device)
         self._zero = torch.zeros(16 * base_channels, dtype=torch.float32, device=self.device)
         mode = os.environ.get("SD_WSPLIT", "all")
@@ -255,6 +259,7 @@ class UNetEngine:
         # (a rebind means new storages; _state_key then only reads the version counters: ~15 us instead of ~70)
         self._watch_inference = any(t.is_inference() for t in self._watch)
         self._bind_id = getattr(self, "_bind_id", 0) + 1
+        self._buf_list = list(bufs.values())
 
     def _s(self):
         return L.stream_handle(self.device)
@@ -267,7 +272,10 @@ class UNetEngine:
         """None when the state cannot be tracked (inference tensors carry no version counter)."""
         if self._watch_inference:
             return None
-        return (self.state_epoch, self._bind_id, tuple([t._version for t in self._watch]))
+        # the BN buffers' storages too: a `.data` swap keeps the tensor object (and its version counter) but moves the
+        # storage, which a bind() would not notice (the parameters live in the flat buffer, whose moves rebind)
+        return (self.state_epoch, self._bind_id, tuple([t._version for t in self._watch]),
+                tuple([b.data_ptr() for b in self._buf_list]))
 
     def pack_weights(self, cached: bool = False):
         """Pack the weights into the kernels' layouts. cached=True (eval-mode inference): skip when the
@@ -524,7 +532,7 @@ class UNetEngine:
                 rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
                 L.call("sd_bn_eval_coeffs", rm.data_ptr(), rv.data_ptr(), g.data_ptr(), b.data_ptr(), cl.cout,
                        BN_EPS, mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
-            zs = self.zstore and dt == L.SD_BF16 and L.call("sd_conv3x3_ex_ok", src, cl.cout) == 1
+            zs = self.zstore and self._zs_ok and dt == L.SD_BF16 and L.call("sd_conv3x3_ex_ok", src, cl.cout) == 1
             if split or zs:
                 hws = t["hws"]
                 L.call("sd_conv3x3_ex_ws", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s) if split else self._wp(cl.off_f),
@@ -679,14 +687,22 @@ class UNetEngine:
             self._conv_fwd_fp8(self.convs[blk + ".1"])
         return ws
 
-    def forward(self, x: torch.Tensor, train: bool):
-        """x: [B, in_channels, H, W] fp32 NCHW on device. Fills the workspace; heads not run."""
+    def forward(self, x: torch.Tensor, train: bool, need_backward: bool | None = None):
+        """x: [B, in_channels, H, W] fp32 NCHW on device. Fills the workspace; heads not run.
+        need_backward (default: train): backward() may follow. An eval-mode forward with need_backward=True (autograd
+        through a model in eval mode) gets the backward buffers and stores the raw conv outputs the backward reads
+        (no BN-applied stores, no graph replay)."""
         B, C, H, W = x.shape
         if C != self.in_channels:
             raise ValueError(f"expected {self.in_channels} input channels, got {C}")
         if self.fp8 and train:
             raise RuntimeError("precision='fp8' is the inference-only forward (BASELINE config 5): call model.eval()")
-        ws = self.workspace(B, H, W, train)
+        if need_backward is None:
+            need_backward = train
+        if self.fp8 and need_backward:
+            raise RuntimeError("precision='fp8' is the inference-only forward: no backward")
+        self._zs_ok = not need_backward
+        ws = self.workspace(B, H, W, train or need_backward)
         ws.fwd_train = train
         if train:  # batch statistics overwrite the BN coefficients; running statistics move
             self.touch_state()
@@ -707,7 +723,7 @@ class UNetEngine:
         # captured into a HIP graph on the second such forward and replayed from the third on (one host call instead
         # of 27-45 ctypes launches; B=1 960x720 forwards were host-bound at ~20 us of GPU time per kernel)
         gkey = None
-        if not train and self.eval_graphs and not self._eval_coeffs and ws.coeff_key is not None:
+        if not need_backward and self.eval_graphs and not self._eval_coeffs and ws.coeff_key is not None:
             gkey = (ws.coeff_key, self._fwd_path(ws))
             if ws.graph is not None and ws.graph_key == gkey:
                 with torch.cuda.device(self.device):  # replays on the current stream of the engine's device
@@ -740,10 +756,23 @@ class UNetEngine:
             s, ev = self._fp8_cal
             ev.synchronize()  # recorded a frame ago: normally complete already
             self._fp8_cal_amax = float(self._amax_host[s])
-        prev = (slot + 2) % 3
-        ev = self._amax_ev[prev]
-        if (self.fp8_range_margin > 0 and self._amax_used[prev] and ev.query() and self._fp8_cal_amax is not None
-                and float(self._amax_host[prev]) > self.fp8_range_margin * self._fp8_cal_amax):
+        # every earlier frame's amax is checked once: the previous frame's when its read-back has landed, the one before
+        # it (ring word `clear`, whose host copy the next frame's read-back overwrites) now, waiting for it if the
+        # caller queued frames faster than they complete (it was recorded two frames ago: normally done already)
+        hit = False
+        for s in ((slot + 1) % 3, (slot + 2) % 3):  # frame f - 2, then f - 1
+            if not self._amax_used[s] or self._amax_checked[s]:
+                continue
+            ev = self._amax_ev[s]
+            if s == (slot + 1) % 3:
+                ev.synchronize()
+            elif not ev.query():
+                continue
+            self._amax_checked[s] = True
+            if (self.fp8_range_margin > 0 and self._fp8_cal_amax is not None
+                    and float(self._amax_host[s]) > self.fp8_range_margin * self._fp8_cal_amax):
+                hit = True
+        if hit:
             self.fp8_range_recalibrations += 1
             return True
         if self.fp8_recalib_every and self._fp8_age >= self.fp8_recalib_every:
@@ -765,6 +794,7 @@ class UNetEngine:
                 self._amax_host = torch.zeros(3, dtype=torch.float32, pin_memory=True)
             self._amax_ev = [torch.cuda.Event() for _ in range(3)]
             self._amax_used = [False] * 3
+            self._amax_checked = [True] * 3
             self._amax_packed = torch.cuda.Event()
         if self._fp8_policy(ws, slot):
             ws.q8_ready = False
@@ -794,6 +824,7 @@ class UNetEngine:
             self._amax_host[slot:slot + 1].copy_(self._amax_dev[slot:slot + 1], non_blocking=True)
             self._amax_ev[slot].record(side)
         self._amax_used[slot] = True
+        self._amax_checked[slot] = False
 
     def _capture(self, ws: Workspace, gkey, train: bool):
         """Capture the forward body into a HIP graph on the engine's OWN capture stream on its device (torch's shared
@@ -1089,6 +1120,9 @@ class UNetEngine:
         """Full backward after heads() wrote da:dec1.1 (model.py:79-104 in reverse).
         grad_hook(name) fires when the gradients of top-level module `name` are final."""
         self.phase = "bwd"
+        if self._zs:
+            raise RuntimeError("backward after a forward that stored BN-applied outputs (an eval forward without "
+                               "need_backward=True): its activations are not the ones the backward reads")
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         for blk in reversed(BLOCKS_FWD):
             if blk in ("enc1", "enc2", "enc3", "enc4"):

@@ -67,7 +67,7 @@ class _UNetFunction(torch.autograd.Function):
         eng = model._engine
         B, _, H, W = x.shape
         eng.pack_weights()
-        eng.forward(x, train=model.training)
+        eng.forward(x, train=model.training, need_backward=True)
         disp = torch.empty(B, 1, H, W, dtype=torch.float32, device=x.device)
         logvar = torch.empty_like(disp)
         eng.heads(L.SD_HEADS_INFER, disp=disp, logvar=logvar)
@@ -145,20 +145,29 @@ class StereoUNet(nn.Module):
     def _named_trainable(self):
         """(state_dict key, Parameter) in backward-production order. The module tree is fixed after construction, so
         the list is built once (rebuilding it took ~0.4 ms of host time per forward, which B=1 inference felt)."""
-        cache = self.__dict__.get("_trainable_cache")  # dropped by _apply (.to() may create new Parameters)
+        cache = self.__dict__.get("_trainable_cache")  # dropped by _apply and by _is_flat when a Parameter moved
         if cache is None:
             named = dict(self.named_parameters())
             cache = []
             for top in GRAD_ORDER:
                 cache.extend((k, p) for k, p in named.items() if k.split(".")[0] == top)
             self.__dict__["_trainable_cache"] = cache
+            # where each Parameter is registered: a replaced Parameter object (load_state_dict(assign=True), or
+            # `module.weight = nn.Parameter(...)`) is noticed by _is_flat without rebuilding the list
+            mods = dict(self.named_modules())
+            self.__dict__["_trainable_slots"] = [(mods[k.rpartition(".")[0]]._parameters, k.rpartition(".")[2], p)
+                                                 for k, p in cache]
         return cache
 
     def _is_flat(self, device) -> bool:
+        named = self._named_trainable()
+        if any(d.get(n) is not p for d, n, p in self.__dict__["_trainable_slots"]):
+            self.__dict__.pop("_trainable_cache", None)  # a Parameter was replaced: new list, new flat buffer
+            return False
         if self._flat_p is None or self._flat_p.device != device:
             return False
         base = self._flat_p.untyped_storage().data_ptr()
-        return all(p.untyped_storage().data_ptr() == base for _, p in self._named_trainable())
+        return all(p.untyped_storage().data_ptr() == base for _, p in named)
 
     def _flatten(self, device):
         # ordinary tensors even when the first forward runs under torch.inference_mode(): inference

@@ -321,3 +321,31 @@ def test_fp8_recalibrates_when_the_input_range_grows():
         for _ in range(3):
             m(bright.to(DEV))
         assert eng.fp8_calibrations == 4  # the age policy: after 2 static forwards
+
+
+def test_fp8_range_check_sees_frames_queued_without_sync():
+    """the range check of a frame whose input amax had not been read back yet when the next frame was
+    queued must still happen. A caller that queues frames without synchronizing gets the recalibration at most two
+    frames after the wide frame (the ring word of frame f - 2 is checked by frame f, waiting for it if needed)."""
+    from stereo_depth_estimation_amd.model import StereoUNet
+
+    st = U.make_state(32, seed=5)
+    m = StereoUNet(base_channels=32, precision="fp8")
+    m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in st.items()})
+    m = m.to(DEV).eval()
+    eng = m.engine()
+    dark = 0.2 * torch.as_tensor(U.make_batch(1, 240, 320, seed=34)["input"]).to(DEV)
+    bright = torch.as_tensor(U.make_batch(1, 240, 320, seed=33)["input"]).to(DEV)
+    with torch.inference_mode():
+        m(dark)  # calibration
+        for _ in range(3):
+            m(dark)
+        m(bright)  # no synchronize anywhere from here on
+        m(dark)
+        m(dark)  # checks the bright frame's ring word (two frames back) at the latest
+        assert eng.fp8_range_recalibrations == 1 and eng.fp8_calibrations == 2, (
+            eng.fp8_range_recalibrations, eng.fp8_calibrations)
+        for _ in range(3):
+            m(dark)
+        torch.cuda.synchronize()
+    assert eng.fp8_range_recalibrations == 1  # each frame is checked once

@@ -836,71 +836,6 @@ def test_convT_split_pack_doubled_k_matches_fp32_weights():
     assert err <= 2.0 ** -7 * float(ref.abs().max()), err
 
 
-@pytest.mark.parametrize("B,H,W,c0,c1,co,bn", [
-    (2, 24, 64, 64, 0, 64, True),     # 8x32 tiles (WRJ 2), two chunks, BN+ReLU gather
-    (1, 36, 96, 72, 0, 128, True),    # ragged last tile row, a partial chunk, two N-blocks
-    (2, 40, 48, 32, 32, 64, False),   # 16x16 tiles (WRJ 1), two sources (a concatenation)
-    (1, 60, 80, 128, 0, 128, True),   # 60x80: the model's 16x16 tiling with a ragged last tile row
-    (1, 20, 16, 40, 24, 192, True),   # one tile per image, ragged chunks of both sources, three N-blocks
-    (3, 17, 160, 64, 64, 64, False),  # 120x160-style 8x32 tiles, many items per block
-])
-def test_conv3x3_weights_in_registers_equal_lds_weights(monkeypatch, B, H, W, c0, c1, co, bn):
-    """k_halo_conv_wr (SD_HALO_WR=1: weights read from L2 into registers, 8x32 / 16x16 tiles) stores bit for bit what the
-    LDS-weight instance stores: the same 16x16x32 MFMAs meet every output pixel in the same tap and chunk order.
-    STORE, STATS (statistics of the stored values) and the SPLIT dgrad epilogue; both match F.conv2d."""
-    lib = L()
-    torch.manual_seed(21)
-    ci = c0 + c1
-    u = torch.randn(B, c0, H, W).to(torch.bfloat16).float()
-    sk = torch.randn(B, c1, H, W).to(torch.bfloat16).float() if c1 else None
-    sc, sh = torch.rand(ci) + 0.5, torch.randn(ci) * 0.2
-    w = (torch.randn(co, ci, 3, 3) / (3 * ci ** 0.5)).to(torch.bfloat16).float()
-    parts = [u] + ([sk] if c1 else [])
-    x = torch.cat(parts, 1)
-    if bn:
-        x = torch.relu(x * sc[None, :, None, None] + sh[None, :, None, None]).to(torch.bfloat16).float()
-    ref = F.conv2d(x, w, padding=1)
-    wp, kpad = _pack3(w, ci, False, "bf16")
-    scd, shd = sc.to(DEV), sh.to(DEV)
-    src = lib.make_src(_nhwc(u, "bf16"), c0, H, W, taps=9, bn0=(scd[:c0].contiguous(), shd[:c0].contiguous()) if bn else None,
-                       src1=_nhwc(sk, "bf16") if c1 else None, c1=c1,
-                       bn1=(scd[c0:].contiguous(), shd[c0:].contiguous()) if bn and c1 else None)
-    res = {}
-    for wr in ("1", "0"):
-        monkeypatch.setenv("SD_HALO_WR", wr)
-        name = lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, H, W, co, lib.SD_EPI_STATS)
-        assert name.startswith("k_halo_conv_wr<") == (wr == "1"), name
-        rows = lib.call("sd_conv_gemm_stat_rows", lib.SD_BF16, B, H, W, co)
-        outs = {}
-        for epi in (lib.SD_EPI_STORE, lib.SD_EPI_STATS):
-            out = torch.full((B * H * W, co), float("nan"), dtype=torch.bfloat16, device=DEV)
-            st = torch.full((rows, co, 2), float("nan"), device=DEV)
-            lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, epi, out.data_ptr(), None, 0,
-                     None, st.data_ptr() if epi == lib.SD_EPI_STATS else None, lib.stream_handle())
-            outs[epi] = (out, st.double().sum(0).cpu())
-        # dgrad of a concatenation: channels < n_split to out0, the rest to out1
-        ns = co // 2 if co % 64 == 0 else co
-        d0 = torch.full((B * H * W, ns), float("nan"), dtype=torch.bfloat16, device=DEV)
-        d1 = torch.full((B * H * W, co - ns), float("nan"), dtype=torch.bfloat16, device=DEV)
-        lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, lib.SD_EPI_SPLIT, d0.data_ptr(),
-                 d1.data_ptr(), ns, None, None, lib.stream_handle())
-        torch.cuda.synchronize()
-        res[wr] = (outs, d0, d1)
-    (o1, a0, a1), (o0, b0, b1) = res["1"], res["0"]
-    for epi in (lib.SD_EPI_STORE, lib.SD_EPI_STATS):
-        assert torch.equal(o1[epi][0], o0[epi][0]), epi
-    assert torch.equal(o1[lib.SD_EPI_STORE][0], o1[lib.SD_EPI_STATS][0])
-    assert torch.equal(a0, b0) and torch.equal(a1, b1)
-    assert torch.equal(torch.cat([a0, a1], 1), o1[lib.SD_EPI_STORE][0])
-    got = _from_nhwc(o1[lib.SD_EPI_STORE][0], B, H, W, co)
-    assert float((got - ref).abs().max()) <= _tol(ref, "bf16")
-    st1, st0 = o1[lib.SD_EPI_STATS][1], o0[lib.SD_EPI_STATS][1]
-    g64 = got.double()
-    for st in (st1, st0):
-        assert torch.allclose(st[:, 0], g64.sum((0, 2, 3)), rtol=1e-5, atol=1e-3)
-        assert torch.allclose(st[:, 1], (g64 * g64).sum((0, 2, 3)), rtol=1e-5, atol=1e-3)
-
-
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,C,H,W", [(3, 6, 24, 32), (2, 7, 10, 14), (1, 6, 5, 7), (2, 8, 16, 20)])
 def test_pack_input_nchw_to_padded_nhwc(prec, B, C, H, W):

@@ -10,6 +10,8 @@ d = Path(sys.argv[1])
 def micro(arm_files):
     rows = {}
     for f in arm_files:
+        if not f.exists():
+            continue
         for line in f.read_text().splitlines():
             m = re.match(r"^(wgrad .*?|\d+x\d+ .*?)[:|] .*?(\d+\.\d+) us", line)
             if m:
