@@ -231,7 +231,7 @@ def pmc_traffic(kernel: str):
         return None, f"profiles/pmc_traffic.json is from another build ({str(d.get('lib_sha256'))[:12]} != {sha[:12]})"
     ks = d.get("kernels", {})
     # rocprofv3 names every template argument; the library's names leave out trailing defaults (k_halo_conv's OAFF)
-    k = ks.get(kernel) or ks.get(kernel[:-1] + ", false>")
+    k = ks.get(kernel) or ks.get(kernel[:-1] + ", false>") or ks.get(kernel[:-1] + ", false, false>")
     if k is None:
         return None, "kernel not in profiles/pmc_traffic.json"
     return k.get("hbm_bytes_per_launch"), f"profiles/pmc_traffic.json (same build, {sha[:12]})"

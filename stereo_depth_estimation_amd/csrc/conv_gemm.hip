@@ -276,7 +276,7 @@ bool sd_halo_fwd_ok(const sd_src& a, int N, int epi);
 bool sd_halo_fwd_shape(int N);
 int sd_halo_fwd_rows(int batch, int H, int W, int N);
 const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns = false, bool wsplit = false,
-                             bool oaff = false);
+                             bool oaff = false, bool raw = false);
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns = nullptr,
                      bool wsplit = false, const float* osc = nullptr, const float* osh = nullptr, void* ws = nullptr,
@@ -298,7 +298,9 @@ int sd_convt_dgrad(const sd_src& a, int batch, int H, int W, const void* wpack, 
 extern "C" const char* sd_conv_gemm_kernel_name(int dtype, const sd_src* a, int batch, int H, int W, int N, int epi) {
     static thread_local char buf[96];
     const long long M = (long long)batch * H * W;
-    if (dtype == SD_BF16 && a && sd_halo_fwd_ok(*a, N, epi)) return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1]);
+    if (dtype == SD_BF16 && a && sd_halo_fwd_ok(*a, N, epi))
+        return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1], false, false, false,
+                                a->xform[0] != SD_BNRELU && (a->chans[1] == 0 || a->xform[1] != SD_BNRELU));
     if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, N, epi)) return sd_convt_fwd_name(*a, N);
     if (dtype == SD_BF16 && a && sd_convt_dgrad_ok(*a, N, epi)) return sd_convt_dgrad_name(*a, N, false);
     if (dtype == SD_BF16 && a && !a->pool) return sd_fast_fwd_name(*a, M, N);
@@ -418,7 +420,8 @@ extern "C" int sd_conv3x3_ex_ok(const sd_src* a, int N) {
 
 extern "C" const char* sd_conv3x3_ex_kernel_name(const sd_src* a, int H, int W, int N, int epi, int flags, int oaff) {
     if (!sd_conv3x3_ex_ok(a, N)) return "";
-    return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1], false, (flags & SD_CONV_WSPLIT) != 0, oaff != 0);
+    return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1], false, (flags & SD_CONV_WSPLIT) != 0, oaff != 0,
+                            a->xform[0] != SD_BNRELU && (a->chans[1] == 0 || a->xform[1] != SD_BNRELU));
 }
 
 extern "C" long long sd_conv3x3_ex_ws_bytes(const sd_src* a, int batch, int H, int W, int N, int epi, int flags) {

@@ -318,7 +318,7 @@ __device__ __forceinline__ int ld_piece(int item) { return (item >> 3) % PPX; }
 // (Weights in registers for the N % 64 layers, each MFMA wave owning 16 output channels over a whole 256-pixel tile
 // with its A fragments read from L2 one chunk ahead, was built in r04 and measured 5-28 % slower than these LDS-weight
 // instances at every N % 64 shape: DESIGN.md §3 r04. Removed in r05.)
-template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF>
+template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF, bool RAW>
 __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
     static_assert(!(OAFF && (STATS || BNS)), "the affine epilogue stores eval-mode outputs (no statistics)");
     constexpr int BN = 32 * NT;
@@ -464,7 +464,7 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
         // weights: byte offset of each piece in chunk 0 (OOB: past the weight rows of this N-block)
         const __amdgpu_buffer_rsrc_t wrs =
             __builtin_amdgcn_make_buffer_rsrc((void*)p.wp, (short)0, p.N * p.kpad * 2, 0x00020000);
-        constexpr bool WDMA = HC_WDMA && M16 && !WCONST && IT == 1;  // weights by LDS-DMA (below)
+        constexpr bool WDMA = HC_WDMA && M16 && IT == 1 && (!WCONST || RAW);  // weights by LDS-DMA (below)
         unsigned woff[W_PER_THREAD];
 #pragma unroll
         for (int i = 0; i < W_PER_THREAD; ++i) {
@@ -586,6 +586,89 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
                     : "memory");
             }
         };
+        if constexpr (RAW) {
+            // ------------------------------------------------- RAW: every source is a raw tensor (the dgrads, the
+            // pooled encoder inputs): the halo goes global -> LDS by LDS-DMA as well, so these loader waves issue
+            // nothing but LDS-DMA (no VGPR loads, no ds_write, no VALU on the data). The M16 halo is piece-major,
+            // [4 pieces][HPX pixels] of 16 B: loader wave w fills piece w, one wave-instruction per 64 consecutive
+            // halo pixels (lane l: pixel 64 i + l), each lane's source the pixel's 16-B piece in the image (out of the
+            // image or past the source's channels: out of range, zeros written, no traffic). Chunk g's halo and
+            // weights are issued at the start of iteration g into buffer g & 1 and waited for (vmcnt(0)) before the
+            // iteration's barrier.
+            static_assert(M16 && PPX == 4 && HPX % 64 == 0 && WDMA, "RAW: the M16 piece-major halo, weights by DMA");
+            constexpr int HI = HPX / 64;  // halo wave-instructions per loader wave and chunk
+            unsigned hg[HI];              // (halo row << 16 | halo col) of this lane's pixels, ~0 past the halo
+#pragma unroll
+            for (int i = 0; i < HI; ++i) {
+                const int px = i * 64 + lane;
+                const int hy = px / p.hw;
+                hg[i] = px < p.nhalo ? ((unsigned)hy << 16) | (unsigned)(px - hy * p.hw) : 0xffffffffu;
+            }
+            int hp[HI];  // image-local pixel of each, -1 outside the image
+            const __bf16 *rb0 = p.a.p0, *rb1 = p.a.p0;
+            int r_pass = 0, r_cc = 0;
+            auto rgeo = [&]() __attribute__((always_inline)) {
+                const bool live = r_pass < my_items;
+                const int sp = slot + (live ? r_pass : 0) * p.gper;
+                const int b = sp / p.tiles, tl = sp - b * p.tiles;
+                const int ty = tl / p.tiles_x;
+                const int h0 = ty * p.th - 1, w0 = (tl - ty * p.tiles_x) * p.tw - 1;
+                rb0 = p.a.p0 + (size_t)b * hw_img * p.a.c0;
+                rb1 = p.a.c1 ? p.a.p1 + (size_t)b * hw_img * p.a.c1 : p.a.p0;
+#pragma unroll
+                for (int i = 0; i < HI; ++i) {
+                    const int h = h0 + (int)(hg[i] >> 16), w = w0 + (int)(hg[i] & 0xffffu);
+                    const bool in = live & (hg[i] != 0xffffffffu) & (h >= 0) & (w >= 0) & (h < p.H) & (w < p.W);
+                    hp[i] = in ? h * p.W + w : -1;
+                }
+            };
+            rgeo();
+            const unsigned lds_h0 = (unsigned)(uintptr_t)smem + (unsigned)(wid_u * HPX * 16);
+            fill_tables();
+            __syncthreads();  // the tables (the MFMA waves meet it before their first chunk)
+            if constexpr (WCONST) {  // chunk c of every item in buffer c (one chunk: in both)
+                dma_w(0);
+                dma_w(1);
+            }
+            for (int g = 0; g < padded; ++g) {
+                if (g < total) {
+                    const int hv = c_lo + r_cc;
+                    const int hc = hv >= ncp ? hv - ncp : hv;  // wsplit: the second pass re-reads the same halo
+                    const bool s1 = hc >= nc0;
+                    const int C = s1 ? p.a.c1 : p.a.c0;
+                    const int cl = (s1 ? hc - nc0 : hc) * CK;
+                    const __amdgpu_buffer_rsrc_t hrs =
+                        __builtin_amdgcn_make_buffer_rsrc((void*)(s1 ? rb1 : rb0), (short)0, hw_img * C * 2, 0x00020000);
+                    const bool cok = cl + wid_u * 8 < C;
+                    const unsigned soff = __builtin_amdgcn_readfirstlane(cl * 2);
+                    const unsigned m0b = __builtin_amdgcn_readfirstlane(lds_h0 + (unsigned)((g & 1) * BUF * 2));
+#pragma unroll
+                    for (int i = 0; i < HI; ++i) {
+                        const unsigned off = (cok & (hp[i] >= 0)) ? (unsigned)(hp[i] * C + wid_u * 8) * 2u : OOB;
+                        unsigned keep;
+                        asm volatile(
+                            "s_mov_b32 %0, m0\n\t"
+                            "s_mov_b32 m0, %2\n\t"
+                            "s_nop 0\n\t"
+                            "buffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+                            "s_mov_b32 m0, %0"
+                            : "=&s"(keep)
+                            : "v"(off), "s"(m0b + (unsigned)i * 1024u), "s"(hrs), "s"(soff)
+                            : "memory");
+                    }
+                    if constexpr (!WCONST) dma_w(g & 1);
+                    if (++r_cc == nchunks) {
+                        r_cc = 0;
+                        ++r_pass;
+                        rgeo();
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+            __syncthreads();  // stats reduction barrier (MFMA waves)
+            return;
+        }
         auto store_w_from = [&](int buf, const uint4 (&wsrc)[W_PER_THREAD]) __attribute__((always_inline)) {
             __bf16* wl = smem + buf * BUF + HALO_ELEMS;
 #pragma unroll
@@ -1366,9 +1449,9 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
     }
 }
 
-template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF = false>
+template <int NT, int RT, int CK, bool STATS, bool WCONST, int IT, bool BNS, bool OAFF = false, bool RAW = false>
 __global__ __launch_bounds__(512) void k_halo_conv(const HFwdArgs p) {
-    halo_conv_body<NT, RT, CK, STATS, WCONST, IT, BNS, OAFF>(p);
+    halo_conv_body<NT, RT, CK, STATS, WCONST, IT, BNS, OAFF, RAW>(p);
 }
 
 // =====================================================================================
@@ -2068,6 +2151,12 @@ static bool halo_xcd_enabled() {
     return on;
 }
 
+// the all-LDS-DMA loaders for launches whose sources are all raw (SD_HALO_RAW=0: register-staged halos, A/B runs)
+static bool halo_raw_enabled() {  // read per call (A/B modes within one process)
+    const char* e = getenv("SD_HALO_RAW");
+    return !(e && atoi(e) == 0);
+}
+
 // loader-wave priority where the loaders run the BN+ReLU transform (SD_HALO_PRIO=0/1/2 forces one, A/B runs)
 static int halo_prio(const sd_src& a) {
     static const int env = [] {
@@ -2209,18 +2298,17 @@ static bool wconst_chunks(int nchunks) {
 }
 
 // the instance as rocprofv3 names it: k_halo_conv<NT, RT, CK, STATS, WCONST> (launch_halo's choice)
-const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns, bool wsplit, bool oaff) {
-    static thread_local char buf[64];
+const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool bns, bool wsplit, bool oaff, bool raw) {
+    static thread_local char buf[96];
     const bool stats = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(c0 + c1, H, W, N, stats);
     const bool wc = wconst_chunks((cdiv(c0, t.ck) + cdiv(c1, t.ck)) * (wsplit ? 2 : 1));
     const bool wconst = t.ck == 8 ? true : (t.ck != 16 && wc);
-    if (oaff)
-        snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, false, %s, %d, false, true>", N == 32 ? 1 : 2, t.rt, t.ck,
-                 wconst ? "true" : "false", t.it);
-    else
-        snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d, %s>", N == 32 ? 1 : 2, t.rt, t.ck,
-                 stats ? "true" : "false", wconst ? "true" : "false", t.it, bns ? "true" : "false");
+    const bool r = raw && halo_raw_enabled() && t.ck == 32 && t.it == 1 && !bns;
+    // every template argument, as rocprofv3 names the instance
+    snprintf(buf, sizeof(buf), "k_halo_conv<%d, %d, %d, %s, %s, %d, %s, %s, %s>", N == 32 ? 1 : 2, t.rt, t.ck,
+             stats && !oaff ? "true" : "false", wconst ? "true" : "false", t.it, bns ? "true" : "false",
+             oaff ? "true" : "false", r ? "true" : "false");
     return buf;
 }
 
@@ -2294,8 +2382,27 @@ static HSplit halo_split_plan(const HTile& t, int nblk, int gper, int nsp, int N
 }
 
 template <int NT, int RT, int CK, int IT = 1>
-static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p, bool bns = false) {
+static void launch_halo(bool stats, bool wconst, dim3 grid, hipStream_t st, const HFwdArgs& p, bool bns = false,
+                        bool raw = false) {
     constexpr bool W0 = CK == 8, W1 = CK != 16;  // the instance for wconst false / true
+    // every source raw (dgrads, pooled encoder inputs): the all-LDS-DMA loaders (k_halo_conv RAW)
+    if constexpr (IT == 1 && CK == 32) {
+        if (raw && !bns) {
+            auto go = [&](auto ST, auto WC, auto OA) {
+                hipLaunchKernelGGL((k_halo_conv<NT, RT, CK, decltype(ST)::v, decltype(WC)::v, 1, false, decltype(OA)::v,
+                                                true>),
+                                   grid, dim3(512), 0, st, p);
+            };
+            auto by_wc = [&](auto ST, auto OA) {
+                if (wconst) go(ST, BoolC<true>{}, OA);
+                else go(ST, BoolC<false>{}, OA);
+            };
+            if (p.osc) by_wc(BoolC<false>{}, BoolC<true>{});
+            else if (stats) by_wc(BoolC<true>{}, BoolC<false>{});
+            else by_wc(BoolC<false>{}, BoolC<false>{});
+            return;
+        }
+    }
     if constexpr (IT == 1 && CK != 16) {
         if (p.osc) {  // eval forwards with the BN affine in the epilogue (sd_conv3x3_ex)
             if (wconst ? W1 : W0)
@@ -2406,23 +2513,25 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
                "sd_conv_gemm(halo): image %dx%d or weights %dx%d too large for 32-bit offsets", H, W, N, kpad);
     const dim3 grid(p.gblk * q.ksplit);
     const bool wc = wconst_chunks(q.cps);
+    const bool raw = halo_raw_enabled() && t.ck == 32 && t.it == 1 && !bns && a.xform[0] != SD_BNRELU &&
+                     (a.chans[1] == 0 || a.xform[1] != SD_BNRELU);
     SD_REQUIRE(!(N == 32 && t.ck == 32 && t.rt == 4) || (t.th == 16 && t.tw == 32),
                "sd_conv_gemm(halo): the N = 32 RT 4 instances (vertical reuse) need 16x32 tiles, got %dx%d", t.th, t.tw);
     SD_REQUIRE(t.ck != 8 || nch == 1, "sd_conv_gemm(halo): CK = 8 needs <= 8 input channels");
     if (q.nt1) {  // 32-channel N-blocks of an N % 64 layer (batch-1 eval)
-        if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p);
-        else launch_halo<1, 2, 32>(st_, wc, grid, st, p);
+        if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p, false, raw);
+        else launch_halo<1, 2, 32>(st_, wc, grid, st, p, false, raw);
     } else if (t.ck == 8) {
         if (t.rt == 4) launch_halo<1, 4, 8>(st_, wc, grid, st, p);
         else if (t.rt == 3) launch_halo<1, 3, 8>(st_, wc, grid, st, p);
         else launch_halo<1, 2, 8>(st_, wc, grid, st, p);
     } else if (N == 32) {
-        if (t.rt == 4) launch_halo<1, 4, 32>(st_, wc, grid, st, p, bns);
-        else if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p, bns);
-        else launch_halo<1, 2, 32>(st_, wc, grid, st, p, bns);
+        if (t.rt == 4) launch_halo<1, 4, 32>(st_, wc, grid, st, p, bns, raw);
+        else if (t.rt == 3) launch_halo<1, 3, 32>(st_, wc, grid, st, p, bns, raw);
+        else launch_halo<1, 2, 32>(st_, wc, grid, st, p, bns, raw);
     } else if (t.ck == 32) {
-        if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p, bns);
-        else launch_halo<2, 2, 32>(st_, wc, grid, st, p, bns);
+        if (t.rt == 3) launch_halo<2, 3, 32>(st_, wc, grid, st, p, bns, raw);
+        else launch_halo<2, 2, 32>(st_, wc, grid, st, p, bns, raw);
     } else if (t.it == 2) {  // RT = 2 only (RT = 3 with two accumulator sets spills)
         launch_halo<2, 2, 16, 2>(st_, wc, grid, st, p);
     } else if (t.rt == 4) {

@@ -858,3 +858,55 @@ def test_pack_input_nchw_to_padded_nhwc(prec, B, C, H, W):
     assert torch.equal(out.cpu(), ref) and torch.equal(out2.cpu(), ref)
     got_max = amax[:1].cpu().view(torch.float32).item()
     assert got_max == float(x.abs().max()) and int(amax[1]) == 0
+
+
+@pytest.mark.parametrize("B,H,W,c0,c1,co", [
+    (2, 24, 64, 64, 0, 64),      # 8x32 tiles, two chunks (weights resident: WCONST)
+    (1, 36, 96, 72, 0, 128),     # ragged last tile row, a partial chunk, two N-blocks
+    (2, 40, 48, 32, 32, 64),     # two raw sources (a ConvTranspose output + another raw tensor)
+    (1, 30, 40, 160, 0, 256),    # 5 chunks: per-chunk weight DMA, four N-blocks
+    (1, 15, 20, 96, 64, 512),    # whole-image tile (RT 3), 5 chunks over two sources
+    (2, 32, 64, 32, 0, 32),      # N = 32, 16x32 tiles (RT 4, vertical reuse)
+    (1, 48, 64, 96, 0, 32),      # N = 32, three chunks
+])
+def test_conv3x3_raw_source_dma_loaders_bit_identical(monkeypatch, B, H, W, c0, c1, co):
+    """k_halo_conv RAW (every source raw: halo and weights by LDS-DMA, no register staging) stores bit for bit what the
+    register-staged loaders store (SD_HALO_RAW=0): the same LDS images, the same MFMA order. STORE, STATS and the SPLIT
+    dgrad epilogue; and the result matches F.conv2d."""
+    lib = L()
+    torch.manual_seed(23)
+    ci = c0 + c1
+    u = torch.randn(B, c0, H, W).to(torch.bfloat16).float()
+    sk = torch.randn(B, c1, H, W).to(torch.bfloat16).float() if c1 else None
+    w = (torch.randn(co, ci, 3, 3) / (3 * ci ** 0.5)).to(torch.bfloat16).float()
+    x = torch.cat([u] + ([sk] if c1 else []), 1)
+    ref = F.conv2d(x, w, padding=1)
+    wp, kpad = _pack3(w, ci, False, "bf16")
+    src = lib.make_src(_nhwc(u, "bf16"), c0, H, W, taps=9, src1=_nhwc(sk, "bf16") if c1 else None, c1=c1)
+    res = {}
+    for raw in ("1", "0"):
+        monkeypatch.setenv("SD_HALO_RAW", raw)
+        name = lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, H, W, co, lib.SD_EPI_STORE)
+        assert name.endswith("true>" if raw == "1" else "false>"), name
+        rows = lib.call("sd_conv_gemm_stat_rows", lib.SD_BF16, B, H, W, co)
+        outs = {}
+        for epi in (lib.SD_EPI_STORE, lib.SD_EPI_STATS):
+            out = torch.full((B * H * W, co), float("nan"), dtype=torch.bfloat16, device=DEV)
+            st = torch.full((rows, co, 2), float("nan"), device=DEV)
+            lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, epi, out.data_ptr(), None, 0,
+                     None, st.data_ptr() if epi == lib.SD_EPI_STATS else None, lib.stream_handle())
+            outs[epi] = (out, st)
+        ns = co // 2
+        d0 = torch.full((B * H * W, ns), float("nan"), dtype=torch.bfloat16, device=DEV)
+        d1 = torch.full((B * H * W, co - ns), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, lib.SD_EPI_SPLIT, d0.data_ptr(),
+                 d1.data_ptr(), ns, None, None, lib.stream_handle())
+        torch.cuda.synchronize()
+        res[raw] = (outs, d0, d1)
+    (o1, a0, a1), (o0, b0, b1) = res["1"], res["0"]
+    for epi in (lib.SD_EPI_STORE, lib.SD_EPI_STATS):
+        assert torch.equal(o1[epi][0], o0[epi][0]), epi
+    assert torch.equal(o1[lib.SD_EPI_STATS][1], o0[lib.SD_EPI_STATS][1])
+    assert torch.equal(a0, b0) and torch.equal(a1, b1)
+    got = _from_nhwc(o1[lib.SD_EPI_STORE][0], B, H, W, co)
+    assert float((got - ref).abs().max()) <= _tol(ref, "bf16")

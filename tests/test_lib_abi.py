@@ -65,21 +65,21 @@ def test_planning_queries_are_host_only():
     # bf16 3x3 convs: one stats row per persistent block (256 blocks split over the N-blocks)
     assert L.call("sd_conv_gemm_stat_rows", L.SD_BF16, 64, 240, 320, 32) == 256
     src = L.make_src(ctypes.c_void_p(16), 32, 240, 320, taps=9)
-    assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, 64, 240, 320, 32, L.SD_EPI_STATS) == "k_halo_conv<1, 4, 32, true, true, 1, false>"  # 16x32 tiles, one chunk
-    assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, 64, 240, 320, 32, L.SD_EPI_STORE) == "k_halo_conv<1, 4, 32, false, true, 1, false>"  # 16x32
+    assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, 64, 240, 320, 32, L.SD_EPI_STATS) == "k_halo_conv<1, 4, 32, true, true, 1, false, false, true>"  # 16x32 tiles, one chunk, raw source: all-DMA loaders
+    assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, 64, 240, 320, 32, L.SD_EPI_STORE) == "k_halo_conv<1, 4, 32, false, true, 1, false, false, true>"  # 16x32
     # 3x3 convs with N % 64 == 0 take the halo kernel too; tile shape follows the image
     assert L.call("sd_conv_gemm_stat_rows", L.SD_BF16, 64, 60, 80, 128) == 128  # 2 N-blocks
     assert L.call("sd_conv_gemm_stat_rows", L.SD_BF16, 64, 15, 20, 512) == 32  # 8 N-blocks
     assert L.call("sd_conv_gemm_stat_rows", L.SD_BF16, 2, 15, 20, 512) == 2  # never more rows than tiles
     src15 = L.make_src(ctypes.c_void_p(16), 256, 15, 20, taps=9)
-    assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src15, 64, 15, 20, 512, L.SD_EPI_STATS) == "k_halo_conv<2, 3, 32, true, false, 1, false>"
+    assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src15, 64, 15, 20, 512, L.SD_EPI_STATS) == "k_halo_conv<2, 3, 32, true, false, 1, false, false, true>"
     assert L.kernel_name("sd_conv_gemm_kernel_name", L.SD_BF16, src, 64, 240, 320, 96, L.SD_EPI_STORE).startswith("k_conv_fwd_bf16<")
     sp = L.call("sd_wgrad_splits", L.SD_BF16, 64, 240, 320, 32, 288)
     assert 1 <= sp <= 64 * 240 * 320 // 256
     assert L.call("sd_chan_reduce_rows", 1000, 32) >= 1
     # dgrads that also sum the BatchNorm backward of the layer they produce da for (not the 15x20 RT 3 tiles)
     assert L.call("sd_conv_gemm_bnsum_ok", L.SD_BF16, src, 32) == 1
-    assert L.kernel_name("sd_conv_gemm_bnsum_kernel_name", src, 240, 320, 32) == "k_halo_conv<1, 4, 32, false, true, 1, true>"
+    assert L.kernel_name("sd_conv_gemm_bnsum_kernel_name", src, 240, 320, 32) == "k_halo_conv<1, 4, 32, false, true, 1, true, false, false>"
     assert L.call("sd_conv_gemm_bnsum_rows", src, 64, 240, 320, 32) == 256
     assert L.call("sd_conv_gemm_bnsum_ok", L.SD_BF16, src15, 512) == 0
     # BatchNorm-backward apply fused into the warp-specialised weight gradients (every 3x3 wgrad but enc1.0's)

@@ -4,7 +4,7 @@
 
 Times forward convs (BN+ReLU gather, STATS epilogue) and dgrad-style convs (plain gather, STORE
 epilogue) at B=64 for each U-Net level with HIP events and prints us/launch and TFLOP/s.
---modes runs each layer once per mode (ck16 / ck32 = SD_HALO_CK, n32x8 = SD_HALO_N32=8); --compare checks that every mode
+--modes runs each layer once per mode (ck16 / ck32 = SD_HALO_CK, n32x8 = SD_HALO_N32=8, raw0 = SD_HALO_RAW=0); --compare checks that every mode
 stores the same outputs as the first (max |diff| relative to max |out|).
 """
 
@@ -182,11 +182,14 @@ def main():
             for mode in modes:
                 os.environ.pop("SD_HALO_CK", None)
                 os.environ.pop("SD_HALO_N32", None)
+                os.environ.pop("SD_HALO_RAW", None)
                 for part in mode.split("+"):
                     if part.startswith("ck"):
                         os.environ["SD_HALO_CK"] = part[2:]
                     elif part.startswith("n32x"):  # N=32 full-res tile rows (SD_HALO_N32)
                         os.environ["SD_HALO_N32"] = part[4:]
+                    elif part == "raw0":  # register-staged halos for raw sources (SD_HALO_RAW=0)
+                        os.environ["SD_HALO_RAW"] = "0"
                 us, name, out, tot = run(B, H, W, ci, co, stats, s, dev)
                 if mode not in best or us < best[mode][0]:
                     best[mode] = (us, name)
