@@ -777,8 +777,8 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
             }
             if (!(WG_EXP & 65536)) load(U);
             stamp(t_ld);
-            if constexpr (WDMA) {  // this chunk's weight DMA landed; the halo loads just issued stay in flight
-                __builtin_amdgcn_sched_barrier(0);
+            if constexpr (WDMA && !(WG_EXP & 4194304)) {  // this chunk's weight DMA landed; the halo loads just issued
+                __builtin_amdgcn_sched_barrier(0);                // stay in flight (WG_EXP bit 22: no wait, timing only)
                 asm volatile("s_waitcnt vmcnt(%0)" ::"i"(IT * HP) : "memory");
             }
             __syncthreads();
