@@ -324,13 +324,6 @@ int sd_fp8_qparams(const sd_qsrc* src, int nsrc, float* act_scale, sd_stream s);
  * channels; a concatenation's first source a multiple of 16 channels). */
 int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
                   const float* act_scale, int N, int kpad, void* out, sd_stream s);
-/* The same with a split-K workspace: where the layer's items would leave most CUs idle (the batch-1 forwards of the
- * deep layers) groups of blocks take slices of the input channels and a second launch adds their fp32 partial sums.
- * ws (16-B aligned) must hold sd_conv3x3_q8_ws_bytes(batch, H, W, N, c0, c1) bytes (0: no split for the shape); a
- * NULL or smaller ws runs the unsplit kernel. Results equal sd_conv3x3_q8's up to fp32 summation order. */
-long long sd_conv3x3_q8_ws_bytes(int batch, int H, int W, int N, int c0, int c1);
-int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
-                     const float* act_scale, int N, int kpad, void* out, void* ws, long long ws_bytes, sd_stream s);
 const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1);
 
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----

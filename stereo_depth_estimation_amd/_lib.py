@@ -163,8 +163,6 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_conv3x3_fp8": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p, _p]),
     "sd_conv3x3_q8": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p]),
     "sd_conv3x3_q8_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
-    "sd_conv3x3_q8_ws_bytes": (ctypes.c_longlong, [_i, _i, _i, _i, _i, _i]),
-    "sd_conv3x3_q8_ws": (_i, [_SRC, _i, _i, _i, _p, _p, _p, _i, _i, _p, _p, ctypes.c_longlong, _p]),
     "sd_conv3x3_fp8_rows": (_i, [_i, _i, _i, _i]),
     "sd_conv3x3_fp8_kernel_name": (ctypes.c_char_p, [_i]),
     "sd_chan_minmax_rows": (_i, [_i64, _i]),

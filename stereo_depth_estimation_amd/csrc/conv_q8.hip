@@ -50,13 +50,6 @@ struct QArgs {
     int N, kpad, ctap;
     __bf16* out;
     int xcd;              // XCD-contiguous block numbering (grid % 8 == 0)
-    // split-K (batch-1 forwards of the deep layers, whose few items leave most CUs idle and run their chunks one after
-    // another): ksplit groups of gblk = gper * nblk blocks, group ks takes chunks [ks*cps, ks*cps + cps) of every item
-    // and stores its dequantised fp32 partial sums to part[ks][pixel][N]; k_q8_split_reduce adds the groups' partials
-    // and stores the bf16 output. ksplit = 1: no partials, the epilogue stores `out`.
-    int ksplit, gblk, cps;
-    int npix;             // batch * H * W (partials rows per split)
-    float* part;
 };
 
 // 16 bf16 channels (lo: 0-7, hi: 8-15) -> 16 e4m3 bytes: med3(y*qs + qh, lo_clamp, 448), lo_clamp = 0 for a ReLU
@@ -109,14 +102,12 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
     const bool is_loader = (tid >> 6) >= 4;
     const int wid = (tid >> 6) & 3;
     const int bid = p.xcd ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-    const int ks = bid / p.gblk, bb = bid - ks * p.gblk;
-    const int nb = bb % p.nblk, slot = bb / p.nblk;
+    const int nb = bid % p.nblk, slot = bid / p.nblk;
     const int n0 = nb * BN;
     // chunks never straddle the two sources (a source's last chunk may be partial)
     const int nc0 = (p.c0 + QC - 1) / QC;
-    const int nch_all = nc0 + (p.c1 + QC - 1) / QC;
-    const int c_lo = ks * p.cps;  // this split's chunks: [c_lo, c_lo + nchunks)
-    const int nchunks = (c_lo + p.cps < nch_all ? c_lo + p.cps : nch_all) - c_lo;
+    const int nchunks = nc0 + (p.c1 + QC - 1) / QC;
+    constexpr int c_lo = 0;
     const int mvalid = p.th * p.tw;
     const int my_items = slot < p.nsp ? (p.nsp - 1 - slot) / p.gper + 1 : 0;
     const int total = my_items * nchunks;
@@ -414,32 +405,6 @@ __global__ __launch_bounds__(512) void k_halo_conv_q8(const QArgs p) {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.out + (size_t)b * hw_img * p.N), (short)0, hw_img * p.N * 2, 0x00020000);
             const int chq = 4 * (lane >> 5);
-            if (p.part) {
-                // split-K partials straight from the C layout: lane = pixel (lane & 31) of tile i, 4 consecutive
-                // channels t*32 + 8*g4 + chq + 0..3 per 16-B store (batch-1 sizes: a few MB per launch)
-                float* const pk = p.part + ((size_t)ks * p.npix + (size_t)b * hw_img) * p.N;
-#pragma unroll
-                for (int i = 0; i < RT; ++i) {
-                    const int m = (wid + 4 * i) * 32 + (lane & 31);
-                    const int hm = m / p.tw, wm = m - hm * p.tw;
-                    const bool live = (m < mvalid) & (h0 + hm < p.H) & (w0 + wm < p.W);
-                    const size_t pix = (size_t)(h0 + hm) * p.W + w0 + wm;
-#pragma unroll
-                    for (int t = 0; t < NT; ++t)
-#pragma unroll
-                        for (int g4 = 0; g4 < 4; ++g4) {
-                            const int c = t * 32 + 8 * g4 + chq;
-                            const float4 d = *reinterpret_cast<const float4*>(deq + c);
-                            if (live && n0 + c < p.N)
-                                *reinterpret_cast<float4*>(pk + pix * p.N + n0 + c) =
-                                    make_float4(acc[i][t][4 * g4] * d.x, acc[i][t][4 * g4 + 1] * d.y,
-                                                acc[i][t][4 * g4 + 2] * d.z, acc[i][t][4 * g4 + 3] * d.w);
-                        }
-                }
-                cc = 0;
-                ++item;
-                continue;
-            }
             // all tiles' scratch writes and read-backs issue back to back, then the stores: one LDS round trip per
             // item (LDS is in order per wave, so a tile's writes land after the previous tile's reads)
             uint4 rows[RT][ER];
@@ -517,25 +482,6 @@ static QTile q8_tile(int H, int W, int N, int nch) {
     return {8, 32, 2};
 }
 
-// sum of the split-K partials (part[ks][pixel][N], fp32) -> bf16 out[pixel][N]: 8 channels per thread, the splits in
-// order (deterministic)
-__global__ __launch_bounds__(256) void k_q8_split_reduce(const float* __restrict__ part, int ksplit, long long n8,
-                                                         __bf16* __restrict__ out) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n8) return;
-    const float4* src = reinterpret_cast<const float4*>(part) + 2 * i;
-    float4 a = src[0], b = src[1];
-    for (int k = 1; k < ksplit; ++k) {
-        const float4 x = src[(size_t)k * 2 * n8], y = src[(size_t)k * 2 * n8 + 1];
-        a.x += x.x, a.y += x.y, a.z += x.z, a.w += x.w;
-        b.x += y.x, b.y += y.y, b.z += y.z, b.w += y.w;
-    }
-    bf16x8 v;
-    v[0] = (__bf16)a.x, v[1] = (__bf16)a.y, v[2] = (__bf16)a.z, v[3] = (__bf16)a.w;
-    v[4] = (__bf16)b.x, v[5] = (__bf16)b.y, v[6] = (__bf16)b.z, v[7] = (__bf16)b.w;
-    reinterpret_cast<bf16x8*>(out)[i] = v;
-}
-
 template <int NT, int RT>
 static void launch_q8(bool wconst, dim3 grid, hipStream_t st, const QArgs& p) {
     if constexpr (RT == 4)
@@ -546,48 +492,27 @@ static void launch_q8(bool wconst, dim3 grid, hipStream_t st, const QArgs& p) {
         hipLaunchKernelGGL((k_halo_conv_q8<NT, RT, false>), grid, dim3(512), 0, st, p);
 }
 
-// launch plan of one conv: tile, N-blocks, blocks per N-block and (split = true) the split-K groups and 32-channel
-// N-blocks of a grid of fewer than 128 blocks. The engine passes no workspace by default (SD_Q8_SPLIT=1 in the engine
-// does): at the live app's 960x720 only the 45x60 bottleneck convs qualify, and their split (2 groups, 192 blocks) saved
-// 4.8 us of kernel against the 5.0 us of the reduce launch (bottleneck.1 30.9 -> 26.1 + 5.0 us, bottleneck.0 19.3 ->
-// 17.0 + 5.0 us). The e4m3 chunks hold 64 channels, so these layers have 4-8 chunks per item against the bf16 path's
-// 16-32 (hi/lo passes of 32-channel chunks), where the same split pays (sd_conv3x3_ex_ws).
+// launch plan of one conv: tile, N-blocks, blocks per N-block. (A split-K form for the batch-1 deep layers, groups of
+// blocks over slices of the input chunks plus a reduce launch, saved 4.8 us of kernel against the 5.0 us of its reduce
+// launch at the live app's 960x720 (r04), so it was removed in r05: the e4m3 chunks hold 64 channels and these layers
+// have only 4-8 chunks per item.)
 struct QPlan {
     QTile t;
-    int nt, nblk, gper, nsp, ksplit, cps, nch;
+    int nt, nblk, gper, nsp, nch;
     bool wconst;
 };
-static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1, bool split) {
+static QPlan q8_plan(int batch, int H, int W, int N, int c0, int c1) {
     QPlan q{};
     q.nch = cdiv(c0, QC) + cdiv(c1, QC);
     q.t = q8_tile(H, W, N, q.nch);
     const long long sp = (long long)batch * cdiv(W, q.t.tw) * cdiv(H, q.t.th);
     q.nsp = sp < (1LL << 30) ? (int)sp : (1 << 30);
-    auto grid_of = [&](int nblk) {
-        q.nblk = nblk;
-        q.gper = QPERSIST / nblk;
-        if (q.gper < 1) q.gper = 1;
-        if (q.gper > q.nsp) q.gper = q.nsp;
-        q.ksplit = 1;
-        q.cps = q.nch;
-        const int gblk = q.gper * nblk;
-        if (split && q.t.rt == 2 && gblk < 128 && q.nch >= 2) {  // up to 256 blocks, every split >= 1 chunk
-            int ks = 256 / gblk;
-            if (ks > q.nch) ks = q.nch;
-            if (ks > 1) {
-                q.cps = cdiv(q.nch, ks);
-                q.ksplit = cdiv(q.nch, q.cps);
-            }
-        }
-    };
     q.nt = N == 32 ? 1 : 2;
-    grid_of(N == 32 ? 1 : N / 64);
-    // 64-channel N-blocks of a few items: 32-channel ones double the blocks
-    if (split && q.nt == 2 && q.t.rt == 2 && q.gper * q.nblk * q.ksplit < 128) {
-        q.nt = 1;
-        grid_of(N / 32);
-    }
-    q.wconst = q.cps <= 2;  // chunk c of every item lands in LDS buffer c: weights staged once per block
+    q.nblk = N == 32 ? 1 : N / 64;
+    q.gper = QPERSIST / q.nblk;
+    if (q.gper < 1) q.gper = 1;
+    if (q.gper > q.nsp) q.gper = q.nsp;
+    q.wconst = q.nch <= 2;  // chunk c of every item lands in LDS buffer c: weights staged once per block
     return q;
 }
 
@@ -598,20 +523,13 @@ int sd_validate_src(const sd_src* s, const char* what);
 extern "C" const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1) {
     static thread_local char buf[64];
     if (batch <= 0 || H <= 0 || W <= 0 || !(N == 32 || (N > 0 && N % 64 == 0)) || c0 <= 0 || c1 < 0) return "";
-    const QPlan q = q8_plan(batch, H, W, N, c0, c1, false);
+    const QPlan q = q8_plan(batch, H, W, N, c0, c1);
     snprintf(buf, sizeof(buf), "k_halo_conv_q8<%d, %d, %s>", q.nt, q.t.rt, q.wconst || q.t.rt == 4 ? "true" : "false");
     return buf;
 }
 
-extern "C" long long sd_conv3x3_q8_ws_bytes(int batch, int H, int W, int N, int c0, int c1) {
-    if (batch <= 0 || H <= 0 || W <= 0 || !(N == 32 || (N > 0 && N % 64 == 0)) || c0 <= 0 || c1 < 0) return 0;
-    const QPlan q = q8_plan(batch, H, W, N, c0, c1, true);
-    return q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
-}
-
-extern "C" int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
-                                const float* act_scale, int N, int kpad, void* out, void* ws, long long ws_bytes,
-                                sd_stream s) {
+extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
+                             const float* act_scale, int N, int kpad, void* out, sd_stream s) {
     if (int e = sd_validate_src(a, "sd_conv3x3_q8")) return e;
     SD_REQUIRE(a->taps == 9 && !a->pool, "sd_conv3x3_q8: needs an unpooled 3x3 source");
     SD_REQUIRE(a->H == H && a->W == W, "sd_conv3x3_q8: source grid %dx%d != %dx%d", a->H, a->W, H, W);
@@ -629,10 +547,7 @@ extern "C" int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const 
                a->chans[0]);
     const int ctap = (ctot + 15) / 16 * 16;
     SD_REQUIRE(kpad % 64 == 0 && kpad >= 9 * ctap, "sd_conv3x3_q8: kpad %d < 9*%d", kpad, ctap);
-    QPlan q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1], true);
-    const long long need = q.ksplit > 1 ? (long long)q.ksplit * batch * H * W * N * 4 : 0;
-    if (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0)  // no (or too small a) workspace: the unsplit plan
-        q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1], false);
+    const QPlan q = q8_plan(batch, H, W, N, a->chans[0], a->chans[1]);
     const QTile t = q.t;
     QArgs p;
     p.p0 = (const __bf16*)a->ptr[0];
@@ -664,12 +579,7 @@ extern "C" int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const 
     p.kpad = kpad;
     p.ctap = ctap;
     p.out = (__bf16*)out;
-    p.gblk = q.gper * q.nblk;
-    p.ksplit = q.ksplit;
-    p.cps = q.cps;
-    p.npix = batch * H * W;
-    p.part = q.ksplit > 1 ? (float*)ws : nullptr;
-    const int grid_n = p.gblk * q.ksplit;
+    const int grid_n = q.gper * q.nblk;
     p.xcd = grid_n % 8 == 0;
     SD_REQUIRE(p.nhalo <= q_halo_cap(t.rt) && t.th * t.tw <= 128 * t.rt && t.th < 64 && t.tw < 512,
                "sd_conv3x3_q8: tile %dx%d", t.th, t.tw);
@@ -684,15 +594,6 @@ extern "C" int sd_conv3x3_q8_ws(const sd_src* a, int batch, int H, int W, const 
     } else {
         launch_q8<2, 2>(q.wconst, grid, to_stream(s), p);
     }
-    if (q.ksplit > 1) {
-        const long long n8 = (long long)batch * H * W * N / 8;
-        hipLaunchKernelGGL(k_q8_split_reduce, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, to_stream(s), p.part,
-                           q.ksplit, n8, p.out);
-    }
     return sd_check_launch("sd_conv3x3_q8");
 }
 
-extern "C" int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, const float* wscale,
-                             const float* act_scale, int N, int kpad, void* out, sd_stream s) {
-    return sd_conv3x3_q8_ws(a, batch, H, W, wq, wscale, act_scale, N, kpad, out, nullptr, 0, s);
-}

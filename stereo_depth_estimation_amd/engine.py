@@ -403,12 +403,6 @@ class UNetEngine:
                     t[f"qh{k}:{cl.name}"] = torch.empty(ch, dtype=f32, device=dev)
             t["mm:xin"] = torch.empty(L.call("sd_chan_minmax_rows", B * H * W, self.cin_pad0), self.cin_pad0, 2,
                                       dtype=f32, device=dev)
-            # split-K partials of the static-scale convs (sd_conv3x3_q8_ws: grids of < 128 blocks), opt-in
-            if os.environ.get("SD_Q8_SPLIT", "0") == "1":
-                q8ws = max([L.call("sd_conv3x3_q8_ws_bytes", B, H >> cl.level, W >> cl.level, cl.cout,
-                                   *(self._fp8_src_chans(cl) + (0,))[:2])
-                            for cl in self.convs.values() if not self._q8_bf16(cl)] + [0])
-                t["q8ws"] = torch.empty(max(q8ws // 4, 4), dtype=f32, device=dev)
             for u in self.ups.values():
                 P = B * (H >> (u.level - 1)) * (W >> (u.level - 1))
                 t["mm:" + u.name] = torch.empty(L.call("sd_chan_minmax_rows", P, u.cout), u.cout, 2, dtype=f32,
@@ -642,10 +636,9 @@ class UNetEngine:
                    None, self._s())
             return
         _, src = self._fp8_src(cl)
-        q8ws = t.get("q8ws")  # split-K workspace: SD_Q8_SPLIT=1 only (it did not pay at 960x720, conv_q8.hip)
-        L.call("sd_conv3x3_q8_ws", src, ws.B, ws.H >> cl.level, ws.W >> cl.level, self.wq8.data_ptr() + cl.off8,
+        L.call("sd_conv3x3_q8", src, ws.B, ws.H >> cl.level, ws.W >> cl.level, self.wq8.data_ptr() + cl.off8,
                self.wscale8.data_ptr() + 4 * cl.soff8, t["as:" + cl.name].data_ptr(), cl.cout, cl.kpad8,
-               t["y:" + cl.name].data_ptr(), L.ptr(q8ws), 0 if q8ws is None else 4 * q8ws.numel(), self._s())
+               t["y:" + cl.name].data_ptr(), self._s())
 
     def _forward_q8(self, ws: Workspace):
         """Static-scale fp8 forward: model state unchanged since the calibration forward (the live app's loop)."""

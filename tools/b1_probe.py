@@ -112,12 +112,9 @@ def main() -> None:
         wsc = torch.full((co,), 1e-2, device=dev)
         asc = torch.ones(1, device=dev)
 
-        wsb = L.call("sd_conv3x3_q8_ws_bytes", 1, H, W, co, ci, 0)
-        qws = torch.empty(max(wsb // 4, 4), device=dev)
-
         def q8():
-            L.call("sd_conv3x3_q8_ws", srcq, 1, H, W, wq.data_ptr(), wsc.data_ptr(), asc.data_ptr(), co, kq,
-                   o.data_ptr(), qws.data_ptr(), 4 * qws.numel(), sp)
+            L.call("sd_conv3x3_q8", srcq, 1, H, W, wq.data_ptr(), wsc.data_ptr(), asc.data_ptr(), co, kq,
+                   o.data_ptr(), sp)
 
         tq = graph_time(q8, reps, s)
         qn = L.kernel_name("sd_conv3x3_q8_kernel_name", 1, H, W, co, ci, 0)
@@ -131,8 +128,8 @@ def main() -> None:
         def q8c():
             i = it[0] % reps
             it[0] += 1
-            L.call("sd_conv3x3_q8_ws", srcs[i], 1, H, W, wqs[i].data_ptr(), wsc.data_ptr(), asc.data_ptr(), co, kq,
-                   os_[i].data_ptr(), qws.data_ptr(), 4 * qws.numel(), sp)
+            L.call("sd_conv3x3_q8", srcs[i], 1, H, W, wqs[i].data_ptr(), wsc.data_ptr(), asc.data_ptr(), co, kq,
+                   os_[i].data_ptr(), sp)
 
         tqc = graph_time(q8c, reps, s)
         print(f"{H:3d}x{W:3d} {ci:3d}->{co:3d}  bf16 {tb:7.2f} us {name}   q8 {tq:7.2f} us  cold {tqc:7.2f} us {qn}")
