@@ -264,8 +264,11 @@ int sd_stat_rows_sum(const float* stats, int rows, int ld, int C, float* out, sd
  *         da[pixels][C] (dtype) = d loss / d act; partials for head grads and metric sums
  * GRADS : da from given dense gdisp/glogvar (autograd path) */
 /* valid pixels of a batch (train.py:329-330: valid_mask & isfinite(target)) into count[0..ncount-1] (1-4 counters, all
- * set to the same value: this rank's count and the loss normaliser that DDP all-reduces, without a copy launch) */
-int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount, sd_stream s);
+ * set to the same value: this rank's count and the loss normaliser that DDP all-reduces, without a copy launch).
+ * clear == NULL: count is zeroed first (a memset); else count must already be zero and the kernel zeroes
+ * clear[0..ncount-1] for the caller's next call (double-buffered counters: one launch per batch). */
+int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount, int* clear,
+                   sd_stream s);
 int sd_heads_rows(int64_t pixels);
 int sd_heads(int dtype, int mode, const void* y, const float* scale, const float* shift, int64_t pixels, int C,
              const float* wd, const float* bd, const float* wl, const float* bl, float* disp, float* logvar,

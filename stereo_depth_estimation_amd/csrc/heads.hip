@@ -337,7 +337,9 @@ __global__ __launch_bounds__(256) void k_heads_finalize(const float* __restrict_
 // 4 pixels per thread per iteration (one 32-bit mask word, one float4 of targets), block
 // reduction, one atomic per block
 __global__ __launch_bounds__(256) void k_count_valid(const float* __restrict__ t, const uint8_t* __restrict__ m,
-                                                     long long P, int* count, int ncount) {
+                                                     long long P, int* count, int ncount, int* clear) {
+    // clear: the other slot of the caller's double-buffered counters, zeroed for its next call (no memset launch)
+    if (clear && blockIdx.x == 0 && threadIdx.x < ncount) clear[threadIdx.x] = 0;
     int c = 0;
     const long long P4 = P / 4;
     auto cnt = [](unsigned mw, float4 tv) {
@@ -426,9 +428,11 @@ int launch_heads(int C, int mode, const void* y, const float* sc, const float* s
 }  // namespace
 
 extern "C" int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount,
-                              sd_stream s) {
+                              int* clear, sd_stream s) {
     SD_REQUIRE(target && mask && count && pixels > 0 && ncount >= 1 && ncount <= 4, "sd_count_valid: bad args");
-    if (hipMemsetAsync(count, 0, sizeof(int) * ncount, to_stream(s)) != hipSuccess) return sd_check_launch("sd_count_valid");
+    SD_REQUIRE(!clear || clear + ncount <= count || count + ncount <= clear, "sd_count_valid: clear overlaps count");
+    if (!clear && hipMemsetAsync(count, 0, sizeof(int) * ncount, to_stream(s)) != hipSuccess)
+        return sd_check_launch("sd_count_valid");
     // one atomic per block and counter, and the same-address atomics serialize (1024 blocks x 2 counters took ~28 us
     // at 320x240 B=64): 256 blocks, each thread with ~18 16-B target loads in passes of four
     long long g = (pixels / 4 + 255) / 256;
@@ -437,7 +441,7 @@ extern "C" int sd_count_valid(const float* target, const uint8_t* mask, int64_t 
     // the vector path needs a 4-B aligned mask and 16-B aligned targets; otherwise scalar-only
     const bool vec = ((uintptr_t)mask % 4 == 0) && ((uintptr_t)target % 16 == 0);
     hipLaunchKernelGGL(k_count_valid, dim3((int)g), dim3(256), 0, to_stream(s), target, mask,
-                       vec ? (long long)pixels : 0LL, count, ncount);
+                       vec ? (long long)pixels : 0LL, count, ncount, clear);
     if (!vec)
         hipLaunchKernelGGL(k_count_valid_scalar, dim3((int)g), dim3(256), 0, to_stream(s), target, mask,
                            (long long)pixels, count, ncount);

@@ -210,10 +210,12 @@ class UNetEngine:
         dev = self.device
         # this rank's valid pixels (metric sums) and the loss normaliser, two ints of one buffer that sd_count_valid
         # fills together (ncount=2); DDP all-reduces `count` alone to the global count (ddp.DataParallel), so the two
-        # never alias and nothing has to copy one into the other
-        self._counts = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.count_local = self._counts[0:1]
-        self.count = self._counts[1:2]
+        # never alias and nothing has to copy one into the other. Two slots of them, alternating per batch: the count
+        # kernel fills one (zero) and zeroes the other for the next batch, so no memset launch precedes it
+        self._counts = torch.zeros(2, 2, dtype=torch.int32, device=dev)
+        self._cslot = 0
+        self.count_local = self._counts[0, 0:1]
+        self.count = self._counts[0, 1:2]
         self.metrics = torch.zeros(5, dtype=torch.float64, device=dev)
         self.adam_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_scratch = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -277,9 +279,11 @@ class UNetEngine:
         return (self.state_epoch, self._bind_id, tuple([t._version for t in self._watch]),
                 tuple([b.data_ptr() for b in self._buf_list]))
 
-    def pack_weights(self, cached: bool = False):
+    def pack_weights(self, cached: bool = False, train: bool = False):
         """Pack the weights into the kernels' layouts. cached=True (eval-mode inference): skip when the
-        parameters are unchanged since the last pack (the live app's forward repeats on fixed weights)."""
+        parameters are unchanged since the last pack (the live app's forward repeats on fixed weights).
+        train=True: the next forward is a training forward, which reads no hi/lo split weights (unless
+        SD_WSPLIT_TRAIN=1), so their pack (a second launch, ~28 us at B=64) is left for the next eval forward."""
         key = self._state_key() if cached else None
         if key is not None and key == self._packed_key:
             return
@@ -320,7 +324,7 @@ class UNetEngine:
             self._split_pack_jobs = (L.SdPackJob * len(sj))(*[L.SdPackJob(*j) for j in sj]) if sj else None
             self._pack_key = key
         L.call("sd_pack_weights", dt, self._pack_jobs, len(self._pack_jobs), base, s)
-        if self._split_pack_jobs is not None:
+        if self._split_pack_jobs is not None and (not train or self.wsplit_train):
             L.call("sd_pack_weights", L.SD_BF16, self._split_pack_jobs, len(self._split_pack_jobs),
                    self.wsplit_pack.data_ptr(), s)
 
@@ -902,8 +906,12 @@ class UNetEngine:
     def count_valid(self, target: torch.Tensor, valid: torch.Tensor):
         """train.py:329-330 valid count, on device: count_local (this rank's pixels, for the
         metric sums) and count (the loss normaliser; DDP all-reduces it to the global count)."""
-        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts.data_ptr(), 2,
-               self._s())
+        k = self._cslot
+        self._cslot ^= 1
+        self.count_local = self._counts[k, 0:1]
+        self.count = self._counts[k, 1:2]
+        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts[k].data_ptr(), 2,
+               self._counts[k ^ 1].data_ptr(), self._s())
 
     # ------------------------------------------------------------------ backward
     @staticmethod

@@ -66,7 +66,7 @@ class _UNetFunction(torch.autograd.Function):
     def forward(ctx, model, x, *params):
         eng = model._engine
         B, _, H, W = x.shape
-        eng.pack_weights()
+        eng.pack_weights(train=model.training)
         eng.forward(x, train=model.training, need_backward=True)
         disp = torch.empty(B, 1, H, W, dtype=torch.float32, device=x.device)
         logvar = torch.empty_like(disp)
@@ -275,7 +275,7 @@ class StereoUNet(nn.Module):
             disp, logvar = _UNetFunction.apply(self, x, *[p for _, p in self._named_trainable()])
         else:
             B, _, H, W = x.shape
-            eng.pack_weights(cached=not self.training)
+            eng.pack_weights(cached=not self.training, train=self.training)
             eng.forward(x, train=self.training)
             disp = torch.empty(B, 1, H, W, dtype=torch.float32, device=x.device)
             logvar = torch.empty_like(disp) if return_uncertainty else None

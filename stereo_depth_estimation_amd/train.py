@@ -61,7 +61,7 @@ def _train_step(model, eng, optimizer, inputs, targets, valid_mask, grad_hook, c
     targets = targets.contiguous()
     eng.count_valid(targets, mask_u8)  # depends on the batch only: counted (and all-reduced) ahead of the forward
     pending = count_hook(eng.count) if count_hook is not None else None
-    eng.pack_weights()
+    eng.pack_weights(train=training)
     eng.forward(inputs, train=training)
     if pending is not None:
         pending.wait()
