@@ -1768,6 +1768,10 @@ __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // tw
 // paces the kernel) stay close to the real halo: HP 34 x 6 rows for 4 x 32 tiles (204 slots), HP 22 x 8
 // rows for tiles up to 6 x 20 (176 slots).
 constexpr int WS_TPX = 128;                     // pixels per tile (4 k-steps)
+// dy tiles by LDS-DMA in the plain (no BatchNorm-backward, single-source-block) instances; WS_DYDMA=0 builds: registers
+#ifndef WS_DYDMA
+#define WS_DYDMA 1
+#endif
 constexpr int WS_PD = 5;                        // tap-steps of fragment read-ahead
 #ifndef WS_PRIO
 // loader waves at s_setprio 1: they run the BN+ReLU (and BatchNorm-backward) transforms and, as the workgroup's younger
@@ -1873,6 +1877,31 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             const unsigned gg = (hgeo[i / 2] >> (16 * (i & 1))) & 0xffffu;
             xpo[i] = (((int)(gg >> 8) - 1) * p.W + (int)(gg & 0xff) - 1) * xC + hc.c;
         }
+        // DYDMA (the plain instances: dy is a raw tensor): the dy tile goes global -> LDS by LDS-DMA. The tile image
+        // is WS_TPX rows of DLD elements (DPP data pieces + 2 pad slots), contiguous, so wave-instruction k fills
+        // slots 64k .. 64k + 63; a lane's slot is (pixel s / RS, piece s % RS), pad slots and pixels past the tile or
+        // the image load out of range (zeros). Issued after the iteration's halo stores into buffer i & 1, waited for
+        // by a counted vmcnt before the barrier (the x loads issued after it stay in flight); hipcc's own counted
+        // waits only grow stricter (it does not see the asm loads). Replaces DYP loads + DYP ds_write_b128 per thread.
+        constexpr bool DYDMA = WS_DYDMA && !BNB && !SPAN && (DLD * 2) % 16 == 0;
+        constexpr int RS = DLD / 8;                             // 16-B slots per tile row
+        constexpr int NDI = (WS_TPX * RS + 63) / 64;            // wave-instructions per tile
+        constexpr int DDI = DYDMA ? (NDI + 3) / 4 : 1;          // per loader wave
+        const int lw = __builtin_amdgcn_readfirstlane(wid);
+        int ddo[DDI];        // element offset from the tile origin in its image, or -1 (pad / past the tile)
+        unsigned ddrc[DDI];  // (row << 8 | col) of the slot's pixel
+        if constexpr (DYDMA) {
+#pragma unroll
+            for (int j = 0; j < DDI; ++j) {
+                const int k = lw * DDI + j, sl = k * 64 + lane;
+                const int m = sl / RS, pc = sl - m * RS;
+                const int hm = m / p.tw, wm = m - hm * p.tw;
+                const bool ok = k < NDI && pc < DPP && m < mvalid && m < WS_TPX;
+                ddo[j] = ok ? (hm * p.W + wm) * p.M + mb + pc * 8 : -1;
+                ddrc[j] = ok ? (unsigned)(hm << 8 | wm) : 0xffffu;
+            }
+        }
+        const unsigned lds_dy0 = (unsigned)(uintptr_t)smem + (unsigned)(lw * DDI) * 1024u;
         // BNB: this thread's 8 dy channels (fixed piece) -> the folded BatchNorm-backward constants
         constexpr int NK = BNB ? 8 : 1;
         float ksc[NK], ksh[NK], kB[NK], kC[NK];
@@ -1927,7 +1956,7 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
             const int dbase = tpx * p.M, xbase = tpx * xC;
             unsigned xm = 0;
 #pragma unroll
-            for (int i = 0; i < DYP; ++i) {
+            for (int i = 0; i < (DYDMA ? 0 : DYP); ++i) {
                 const unsigned rc = (dyrc[i / 2] >> (16 * (i & 1))) & 0xffffu;
                 const bool ok = (rc != 0xffffu) & ((int)(rc >> 8) < rhi - 1) & ((int)(rc & 0xff) < chi - 1) & (rhi > rlo);
                 const unsigned off = ok ? (unsigned)(dbase + dpo[i]) * 2u : OOB;
@@ -1982,7 +2011,7 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
                     const unsigned off = (ok & q.wr) ? (unsigned)(q.dbase + dpo[i]) * 2u : OOB;
                     if (!(WG_EXP & 1048576)) __builtin_amdgcn_raw_buffer_store_b128(data, rdo, off, 0, WS_ST_AUX);
                 }
-            } else {
+            } else if constexpr (!DYDMA) {
 #pragma unroll
                 for (int i = 0; i < DYP; ++i)  // out-of-range pieces were loaded as zeros
                     *reinterpret_cast<uint4*>(dys + (dpix0 + (256 / DPP) * i) * DLD + dpiece * 8) = q.d[i];
@@ -1999,12 +2028,51 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
         // a load or a wait on only some paths makes the compiler's vmcnt bookkeeping drain every load
         constexpr bool DG = (WG_EXP & 1024) != 0;
         unsigned long long t_st = 0, t_ld = 0, t_br = 0, t0 = 0, t1 = 0, t_all = DG ? __builtin_amdgcn_s_memtime() : 0;
+        // DYDMA: tile `tile`'s dy -> LDS buffer buf
+        auto dma_dy = [&](int buf, int tile) __attribute__((always_inline)) {
+            const int tx = tile % p.tiles_x;
+            const int rest = tile / p.tiles_x;
+            const int ty = rest % p.tiles_y, b = rest / p.tiles_y;
+            const int h0 = ty * p.th, w0 = tx * p.tw;
+            const int nimg = p.H * p.W;
+            const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(p.dy + (size_t)b * nimg * p.M), (short)0, nimg * p.M * 2, 0x00020000);
+            int rhi = p.H - h0, chi = p.W - w0;  // tile rows / columns inside the image
+            if (tile >= t_begin + ntile) rhi = 0;  // past the block's range: nothing loaded
+            const int dbase = (h0 * p.W + w0) * p.M;
+            const unsigned m0b = __builtin_amdgcn_readfirstlane(lds_dy0 + (unsigned)(buf * BUF * 2));
+#pragma unroll
+            for (int j = 0; j < DDI; ++j) {
+                if (NDI % 4 != 0 && lw * DDI + j >= NDI) break;  // wave-uniform
+                const bool ok = (ddo[j] >= 0) & ((int)(ddrc[j] >> 8) < rhi) & ((int)(ddrc[j] & 0xffu) < chi);
+                const unsigned off = ok ? (unsigned)(dbase + ddo[j]) * 2u : OOB;
+                unsigned keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\t"
+                    "s_mov_b32 m0, %2\n\t"
+                    "s_nop 0\n\t"
+                    "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                    "s_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "v"(off), "s"(m0b + (unsigned)j * 1024u), "s"(rdy)
+                    : "memory");
+            }
+        };
         auto iter = [&](TSet& q, int buf, int tile) __attribute__((always_inline)) {
             if (DG) t0 = __builtin_amdgcn_s_memtime();
             store(q, buf);
             if (DG) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); t1 = __builtin_amdgcn_s_memtime(); t_st += t1 - t0; }
+            if constexpr (DYDMA) {
+                __builtin_amdgcn_sched_barrier(0);
+                dma_dy(buf, tile - 2);  // the tile this iteration stages (the set was loaded two iterations ago)
+                __builtin_amdgcn_sched_barrier(0);
+            }
             load(q, tile);
             if (DG) { t0 = t1; t1 = __builtin_amdgcn_s_memtime(); t_ld += t1 - t0; t0 = t1; }
+            if constexpr (DYDMA) {  // this tile's dy landed; the x loads just issued stay in flight
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"i"(HXP) : "memory");
+            }
             __syncthreads();
             if (DG) t_br += __builtin_amdgcn_s_memtime() - t0;
         };

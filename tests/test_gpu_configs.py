@@ -180,6 +180,11 @@ def test_c5_960x720_eval_forward_fp32_bf16_fp8_vs_oracle():
         out[prec] = (d.cpu(), lv.cpu())
     assert float((out["fp32"][0] - d_ref).abs().max()) < 1e-3
     assert float((out["fp32"][1] - lv_ref).abs().max()) < 1e-3
+    # the worst pixel too: bf16's max per-pixel |Δ| within the reference autocast's own max on the
+    # same pairs (measured r05: 0.58 vs 1.17 px at val240, 0.88 vs 2.34 px at val720; tools/bf16_outliers.py puts the
+    # outliers where the logvar head saturates at its clamp, 3.0, with the deviation growing through the decoder)
+    gmax, amax = float((out["bf16"][0] - d_ref).abs().max()), float((d_ac - d_ref).abs().max())
+    assert gmax <= amax, (gmax, amax)
     _assert_within("bf16 disp", out["bf16"][0], d_ref, d_ac, 1.0, 1.0)
     _assert_within("bf16 logvar", out["bf16"][1], lv_ref, lv_ac, 1.0, 1.0)
     _assert_within("fp8 disp", out["fp8"][0], d_ref, d_ac, 6.0, 4.0)
@@ -338,6 +343,11 @@ def test_epe_on_reference_trained_checkpoint(golden_dir, name):
           f"{float((d_ac - d_ref).abs().mean()):.3g}")
     assert float((out["fp32"][0] - d_ref).abs().max()) < 1e-3
     assert float((out["fp32"][1] - lv_ref).abs().max()) < 1e-3
+    # the worst pixel too: bf16's max per-pixel |Δ| within the reference autocast's own max on the
+    # same pairs (measured r05: 0.58 vs 1.17 px at val240, 0.88 vs 2.34 px at val720; tools/bf16_outliers.py puts the
+    # outliers where the logvar head saturates at its clamp, 3.0, with the deviation growing through the decoder)
+    gmax, amax = float((out["bf16"][0] - d_ref).abs().max()), float((d_ac - d_ref).abs().max())
+    assert gmax <= amax, (gmax, amax)
     for k in ref:
         assert abs(epe["fp32"][k] - ref[k]) < 1e-5 * max(1.0, abs(ref[k])), (k, epe["fp32"][k], ref[k])
     mean_disp = float(d_ref.abs().mean())
