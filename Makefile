@@ -10,7 +10,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 
 all: $(LIB)
 
-build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/common.h include/stereo_hip.h
+build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/common.h $(PKG)/csrc/halo_util.h include/stereo_hip.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

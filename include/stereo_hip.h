@@ -329,6 +329,21 @@ int sd_conv3x3_q8(const sd_src* a, int batch, int H, int W, const void* wq, cons
                   const float* act_scale, int N, int kpad, void* out, sd_stream s);
 const char* sd_conv3x3_q8_kernel_name(int batch, int H, int W, int N, int c0, int c1);
 
+/* ---- fused backward of a full-resolution 32 -> 32 conv + BatchNorm + ReLU layer (model.py:36-41: enc1.1, dec1.1)
+ * One pass over the layer: dy = BatchNorm-backward(da, y) (scale, shift, mean, invstd: this layer's forward
+ * coefficients, coef: its [C][3] backward coefficients from sd_bn_bwd_finalize), never stored; the weight gradient as
+ * split-K slabs slab[splits][32][288] (k = tap*32 + ci, reduced by sd_wgrad_reduce with SD_W_CONV3); dx = the dgrad
+ * (wd: sd_pack_conv3_w dgrad layout, kpad >= 288) into dx, which is da of the previous BatchNorm layer, whose raw
+ * output yp and coefficients (pscale, pshift: x = relu(pscale*yp + pshift); pmean, pinvstd) it takes; and that
+ * layer's BatchNorm-backward sums (sum dz, sum dz*xhat) as partials[splits][32] float2, for sd_bn_bwd_finalize.
+ * Replaces sd_wgrad_gemm_bnbwd + sd_conv_gemm_bnsum for these layers. splits = sd_conv3x3_bwd_fused_splits(...). */
+int sd_conv3x3_bwd_fused_ok(int C, int Cx, int H, int W);
+int sd_conv3x3_bwd_fused_splits(int batch, int H, int W);
+int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* scale, const float* shift, const float* mean,
+                         const float* invstd, const float* coef, const void* yp, const float* pscale,
+                         const float* pshift, const float* pmean, const float* pinvstd, const void* wd, int kpad,
+                         int batch, int H, int W, void* dx, float* slab, float* partials, sd_stream s);
+
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----
  * One flat fp32 parameter/gradient/state buffer (all tensors share lr/betas/eps/wd).
  * The step is skipped (and *step not advanced) when *count == 0 (train.py:331-332). */

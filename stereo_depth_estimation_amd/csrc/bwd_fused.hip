@@ -1,0 +1,380 @@
+// Fused backward of a full-resolution 32 -> 32 channel 3x3 conv + BatchNorm + ReLU layer (model.py:36-41; enc1.1 and
+// dec1.1 of the 320x240 StereoUNet, whose tensors are 315 MB each at B = 64). One pass over the layer produces
+//   dy = BatchNorm-backward(da, y)        staged in LDS as a halo, never stored (bn_bwd_pk)
+//   dW = sum_px x[px + tap] dy[px]^T      x = relu(bn_prev(y_prev)), split-K partial slab per block
+//   dx = sum_tap dy[px + tap] Wd[tap]     the dgrad (Wd: the dgrad-packed, flipped weights) = da of the previous
+//                                         BatchNorm layer, stored
+//   the previous layer's BatchNorm-backward sums (sum dz, sum dz*xhat over dx and y_prev), one partial row per block
+// It replaces the fused BatchNorm-backward weight gradient (k_halo_wgrad_ws<32, 32, ..., BNB>: read da, y, y_prev,
+// wrote dy) and the BatchNorm-sums dgrad (k_halo_conv<1, 4, 32, ..., BNS>: read dy, y_prev, wrote dx): per layer
+// 4 full-resolution tensor passes (da, y, y_prev in; dx out) instead of 7.
+//
+// One 512-thread block per CU, persistent over a contiguous range of 4x32-pixel tiles (its split-K range):
+//   waves 4-7 (loaders): per tile, the 6x34 halo of (da, y) -> dy and of y_prev -> x (BN + ReLU), through registers
+//                        (two tiles in flight) into an LDS double buffer, plus the raw y_prev of the tile's interior
+//                        (for the sums);
+//   waves 0-3 (MFMA)   : weight gradient (16 co x 16 ci per wave, v_mfma_f32_16x16x32_bf16 on transposed fragments,
+//                        k = tile pixels) and dgrad (one 32-pixel tile row per wave, all 32 ci, 32x32x16 MFMAs over
+//                        9 taps x 32 dy channels with the dgrad weights resident in LDS), then the dgrad epilogue.
+#include <stdio.h>
+
+#include "halo_util.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int FB_TH = 4, FB_TW = 32;               // output tile
+constexpr int FB_HW = FB_TW + 2, FB_HH = FB_TH + 2;  // halo width / rows
+constexpr int FB_HPX = FB_HW * FB_HH;              // 204 halo pixels
+constexpr int FB_NI = 4;                           // loader items per thread (4 x 256 >= 204 pixels x 4 pieces)
+constexpr int FB_DL = 40;                          // dy halo pixel pitch (80 B: odd 16-B slot count, b128 reads)
+constexpr int FB_XL = 48;                          // x halo pixel pitch (96 B: conflict-free transposed reads)
+constexpr int FB_SL = 40;                          // raw y_prev stash pitch
+constexpr int FB_WL = 9 * 32 + 8;                  // dgrad weight row (592 B, odd slot count)
+constexpr int FB_DYH = 256 * FB_DL, FB_XH = 256 * FB_XL, FB_ST = FB_TH * FB_TW * FB_SL;
+constexpr int FB_BUF = FB_DYH + FB_XH + FB_ST;     // elements per LDS buffer
+constexpr int FB_BLOCKS = 256;                     // one per CU
+
+struct BwdArgs {
+    const __bf16 *da, *y, *yp;                        // [B*H*W][32]
+    const float *sc, *sh, *mu, *is, *coef;            // this layer's BatchNorm: forward affine, statistics, backward coef
+    const float *psc, *psh, *pmu, *pis;               // the previous BatchNorm layer (x = relu(psc*yp + psh))
+    const __bf16* wd;                                 // dgrad-packed weights [32 ci][kpad], k = tap*32 + co (flipped)
+    int kpad;
+    int B, H, W, tiles_x, tiles_y, ntiles, tps;       // tps: tiles per block (its split-K range)
+    __bf16* dx;                                       // [B*H*W][32]
+    float* slab;                                      // [blocks][32 co][288], k = tap*32 + ci
+    float2* part;                                     // [blocks][32] (sum dz, sum dz*xhat) of the previous layer
+};
+
+template <int PPX>
+__device__ __forceinline__ int fb_pixel(int item) { return (item / (8 * PPX)) * 8 + (item & 7); }
+template <int PPX>
+__device__ __forceinline__ int fb_piece(int item) { return (item >> 3) % PPX; }
+
+__global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * FB_BUF];
+    __shared__ __attribute__((aligned(16))) __bf16 wds[32 * FB_WL];
+    __shared__ __attribute__((aligned(16))) __bf16 scr[4 * 32 * 32];  // per-wave dgrad epilogue transpose
+    __shared__ __attribute__((aligned(16))) float redf[4 * 32 * 2];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool is_loader = tid >= 256;
+    const int wid = (tid >> 6) & 3;
+    // XCD-contiguous block numbering: the tile ranges of one XCD's blocks are neighbours (shared halo rows in its L2)
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int t_begin = bid * p.tps;
+    const int ntile = max(0, min(p.ntiles, t_begin + p.tps) - t_begin);
+    const int hw = p.H * p.W;
+
+    // the dgrad weights, resident for the launch (all threads; before the first barrier)
+    for (int i = tid; i < 32 * 36; i += 512) {
+        const int r = i / 36, c8 = i - r * 36;
+        *reinterpret_cast<uint4*>(wds + r * FB_WL + c8 * 8) =
+            *reinterpret_cast<const uint4*>(p.wd + (size_t)r * p.kpad + c8 * 8);
+    }
+
+    if (is_loader) {
+        // =========================================================== loader waves
+        const int ltid = tid - 256;
+        const int piece = fb_piece<4>(ltid);  // fixed per thread (256 * i keeps (item >> 3) % 4)
+        constexpr unsigned OOB = 0x80000000u;
+        // this thread's 8 channels: this layer's folded BatchNorm-backward constants and the previous layer's affine
+        float ksc[8], ksh[8], kB[8], kC[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = piece * 8 + j;
+            const float k1 = p.coef[3 * c + 1], k2 = p.coef[3 * c + 2], is = p.is[c], sc = p.sc[c], sh = p.sh[c];
+            ksc[j] = sc;
+            ksh[j] = sh;
+            kB[j] = -is * k2;
+            kC[j] = is * k2 * sh + sc * (p.mu[c] * is * k2 - k1);
+        }
+        const float4 s0 = *reinterpret_cast<const float4*>(p.psc + piece * 8);
+        const float4 s1 = *reinterpret_cast<const float4*>(p.psc + piece * 8 + 4);
+        const float4 t0 = *reinterpret_cast<const float4*>(p.psh + piece * 8);
+        const float4 t1 = *reinterpret_cast<const float4*>(p.psh + piece * 8 + 4);
+        // halo geometry of the items: (row << 8 | col), ~0 past the halo; interior stash slot or -1
+        unsigned geo[FB_NI];
+        int stash[FB_NI];
+#pragma unroll
+        for (int i = 0; i < FB_NI; ++i) {
+            const int px = fb_pixel<4>(ltid + 256 * i);
+            const int hy = px / FB_HW, hx = px - hy * FB_HW;
+            geo[i] = px < FB_HPX ? (unsigned)(hy << 8 | hx) : 0xffffffffu;
+            const bool in = px < FB_HPX && hy >= 1 && hy <= FB_TH && hx >= 1 && hx <= FB_TW;
+            stash[i] = in ? ((hy - 1) * FB_TW + hx - 1) * FB_SL + piece * 8 : -1;
+        }
+        struct Set {
+            uint4 a[FB_NI], y[FB_NI], x[FB_NI];
+            unsigned m;  // bit i: item i inside the image
+        };
+        Set sa, sb;
+        auto load = [&](Set& q, int tile) __attribute__((always_inline)) {
+            const bool live = tile < t_begin + ntile;
+            const int tl = live ? tile : t_begin;
+            const int tx = tl % p.tiles_x, r = tl / p.tiles_x;
+            const int ty = r % p.tiles_y, b = r / p.tiles_y;
+            const int h0 = ty * FB_TH - 1, w0 = tx * FB_TW - 1;
+            const size_t img = (size_t)b * hw * 32;
+            const __amdgpu_buffer_rsrc_t ra =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(p.da + img), (short)0, hw * 64, 0x00020000);
+            const __amdgpu_buffer_rsrc_t ry =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + img), (short)0, hw * 64, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rp =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(p.yp + img), (short)0, hw * 64, 0x00020000);
+            unsigned m = 0;
+#pragma unroll
+            for (int i = 0; i < FB_NI; ++i) {
+                const int h = h0 + (int)(geo[i] >> 8), w = w0 + (int)(geo[i] & 0xffu);
+                const bool ok = live & (geo[i] != 0xffffffffu) & (h >= 0) & (h < p.H) & (w >= 0) & (w < p.W);
+                m |= (unsigned)ok << i;
+                const unsigned off = ok ? (unsigned)(h * p.W + w) * 64u + (unsigned)piece * 16u : OOB;
+                const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+                const auto vy = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+                const auto vp = __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0);
+                q.a[i] = make_uint4(va[0], va[1], va[2], va[3]);
+                q.y[i] = make_uint4(vy[0], vy[1], vy[2], vy[3]);
+                q.x[i] = make_uint4(vp[0], vp[1], vp[2], vp[3]);
+            }
+            q.m = m;
+        };
+        auto store = [&](Set& q, int buf) __attribute__((always_inline)) {
+            __bf16* dyh = smem + buf * FB_BUF;
+            __bf16* xh = dyh + FB_DYH;
+            __bf16* st = xh + FB_XH;
+#pragma unroll
+            for (int i = 0; i < FB_NI; ++i) {
+                const bool ok = (q.m >> i) & 1u;
+                const int px = fb_pixel<4>(ltid + 256 * i);  // < 256: inside the regions (items past the halo unused)
+                uint4 d = bn_bwd_pk(q.a[i], q.y[i], ksc, ksh, kB, kC);
+                d = ok ? d : make_uint4(0, 0, 0, 0);  // the dgrad's zero padding, and dy past the image
+                uint4 x = bnrelu_pk(q.x[i], s0, s1, t0, t1);
+                x = ok ? x : make_uint4(0, 0, 0, 0);
+                *reinterpret_cast<uint4*>(dyh + px * FB_DL + piece * 8) = d;
+                *reinterpret_cast<uint4*>(xh + px * FB_XL + piece * 8) = x;
+                if (stash[i] >= 0) *reinterpret_cast<uint4*>(st + stash[i]) = q.x[i];  // raw y_prev (0 past the image)
+            }
+        };
+        load(sa, t_begin);
+        __builtin_amdgcn_sched_barrier(0);
+        load(sb, t_begin + 1);
+        __syncthreads();  // the resident weights (the MFMA waves meet it before their first tile)
+        // an even number of iterations (no exit between the two register sets); an odd count's last one stores a
+        // tile past the range into the buffer the MFMA waves no longer read
+        for (int i = 0; i < ntile; i += 2) {
+            store(sa, 0);
+            load(sa, t_begin + i + 2);
+            __syncthreads();
+            store(sb, 1);
+            load(sb, t_begin + i + 3);
+            __syncthreads();
+        }
+        __syncthreads();  // the statistics reduction (MFMA waves)
+        return;
+    }
+
+    // =============================================================== MFMA waves
+    __syncthreads();  // the resident weights
+    // weight gradient: wave (wc, wo) owns ci 16 wc .. +15 and co 16 wo .. +15 (the k_halo_wgrad_ws<32, 32> grid);
+    // transposed fragments: within a 16-lane group, lane 4q + pp supplies row q of pixel rows pc, pc + 8
+    const int g = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
+    const int pc = 16 * (g >> 1) + 4 * (g & 1) + q4;
+    const int ci0 = 16 * (wid & 1), co0 = 16 * (wid >> 1);
+    f32x4 accw[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) accw[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dgrad epilogue: this lane's 8 channels (lane % 4) of the previous BatchNorm layer, for its sums
+    BnsK bk[4];
+    {
+        const int c = (lane & 3) * 8;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float v[4][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ch = c + 2 * q + h;
+                v[0][h] = p.psc[ch];
+                v[1][h] = p.psh[ch];
+                v[2][h] = p.pis[ch];
+                v[3][h] = -p.pmu[ch] * p.pis[ch];
+            }
+            bk[q].sc = f32x2{v[0][0], v[0][1]};
+            bk[q].sh = f32x2{v[1][0], v[1][1]};
+            bk[q].is = f32x2{v[2][0], v[2][1]};
+            bk[q].nmi = f32x2{v[3][0], v[3][1]};
+        }
+    }
+    float own[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) own[j] = 0.f;
+    __bf16* const scw = scr + wid * 32 * 32;
+    auto swz = [](int j, int px) { return j ^ ((px >> 1) & 3); };
+    for (int it = 0; it < ntile; ++it) {
+        __syncthreads();  // tile it is in buffer it & 1
+        const __bf16* dyh = smem + (it & 1) * FB_BUF;
+        const __bf16* xh = dyh + FB_DYH;
+        const __bf16* st = xh + FB_XH;
+        // ---- weight gradient: k = the tile's pixels, 4 k-steps of one 32-pixel tile row each
+#pragma unroll
+        for (int ks = 0; ks < FB_TH; ++ks) {
+            const __bf16* a0 = dyh + ((ks + 1) * FB_HW + 1 + pc) * FB_DL + co0 + 4 * pp;  // dy^T of tile row ks
+            const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
+            bf16x8 bf[9];
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const __bf16* x0 = xh + ((ks + tap / 3) * FB_HW + tap % 3 + pc) * FB_XL + ci0 + 4 * pp;
+                bf[tap] = tr_pair(x0, x0 + 8 * FB_XL);
+            }
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+                accw[tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[tap], accw[tap], 0, 0, 0);
+        }
+        // ---- dgrad of tile row `wid`: C^T[ci][px] over 9 taps x 2 k-steps of 16 dy channels
+        f32x16 accd;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accd[r] = 0.f;
+        const int c8 = 8 * (lane >> 5);
+        const __bf16* wrow = wds + (lane & 31) * FB_WL + c8;
+        const __bf16* drow = dyh + (wid * FB_HW + (lane & 31)) * FB_DL + c8;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int toff = ((tap / 3) * FB_HW + tap % 3) * FB_DL;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + tap * 32 + kk * 16);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(drow + toff + kk * 16);
+                accd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, accd, 0, 0, 0);
+            }
+        }
+        // ---- dgrad epilogue: lanes l / l + 32 hold the 4-channel halves of each 8-channel group of pixel l & 31;
+        // v_permlane32_swap pairs them into whole 16-B pieces, which go through the wave's scratch and leave as
+        // pixel rows (16 pixels x 4 pieces per store instruction), with the previous layer's BatchNorm-backward sums
+        {
+            uint2 pk[4];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                bf16x4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = (__bf16)accd[4 * g4 + q];
+                pk[g4] = *reinterpret_cast<uint2*>(&v);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k += 2) {
+                const auto rx = __builtin_amdgcn_permlane32_swap(pk[k].x, pk[k + 1].x, false, false);
+                const auto ry = __builtin_amdgcn_permlane32_swap(pk[k].y, pk[k + 1].y, false, false);
+                const int px = lane & 31, j = k + (lane >> 5);
+                *reinterpret_cast<uint4*>(scw + px * 32 + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+            }
+            asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
+            const int tl = t_begin + it;
+            const int tx = tl % p.tiles_x, r = tl / p.tiles_x;
+            const int ty = r % p.tiles_y, b = r / p.tiles_y;
+            const int h = ty * FB_TH + wid, w0 = tx * FB_TW;
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(p.dx + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
+            uint4 vv[2], yv[2];
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const int px = rr * 16 + (lane >> 2), j = lane & 3;
+                vv[rr] = *reinterpret_cast<const uint4*>(scw + px * 32 + swz(j, px) * 8);
+                yv[rr] = *reinterpret_cast<const uint4*>(st + (wid * FB_TW + px) * FB_SL + j * 8);
+            }
+            asm volatile("" ::: "memory");  // the next tile's scratch writes after these reads
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const int px = rr * 16 + (lane >> 2), j = lane & 3;
+                const bool live = (h < p.H) & (w0 + px < p.W);
+                bns_add(own, vv[rr], yv[rr], live, bk);
+                __attribute__((ext_vector_type(4))) unsigned data = {vv[rr].x, vv[rr].y, vv[rr].z, vv[rr].w};
+                const unsigned off = live ? (unsigned)(h * p.W + w0 + px) * 64u + (unsigned)j * 16u : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(data, rd, off, 0, 2);
+            }
+        }
+    }
+    if (ntile & 1) __syncthreads();  // the loaders' last (even-count) iteration
+
+    // weight-gradient partial slab: slab[bid][co][tap * 32 + ci]   (16x16 C layout: row 4 (lane >> 4) + r, col lane & 15)
+    float* slab = p.slab + (size_t)bid * 32 * 288;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            slab[(size_t)(co0 + 4 * (lane >> 4) + r) * 288 + tap * 32 + ci0 + (lane & 15)] = accw[tap][r];
+    // the previous layer's BatchNorm-backward sums: lanes l, l + 4, ... hold the same 8 channels
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+        for (int o = 4; o < 64; o <<= 1) own[k] += __shfl_xor(own[k], o);
+    if (lane < 4) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)  // k: channel k / 2, {sum, sum*xhat} k & 1 (bns_add's layout)
+            redf[(wid * 32 + lane * 8 + k / 2) * 2 + (k & 1)] = own[(k & ~3) | ((k & 1) << 1) | ((k >> 1) & 1)];
+    }
+    __syncthreads();
+    if (tid < 32) {
+        float s = 0.f, sx = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            s += redf[(w * 32 + tid) * 2];
+            sx += redf[(w * 32 + tid) * 2 + 1];
+        }
+        p.part[(size_t)bid * 32 + tid] = make_float2(s, sx);
+    }
+}
+
+}  // namespace
+
+extern "C" int sd_conv3x3_bwd_fused_ok(int C, int Cx, int H, int W) {
+    return C == 32 && Cx == 32 && H % FB_TH == 0 && W % FB_TW == 0 && W / FB_TW < 256 && (long long)H * W * 64 < (1LL << 31)
+               ? 1
+               : 0;
+}
+
+extern "C" int sd_conv3x3_bwd_fused_splits(int batch, int H, int W) {
+    const long long nt = (long long)batch * (H / FB_TH) * (W / FB_TW);
+    return nt < FB_BLOCKS ? (int)((nt + 7) / 8 * 8) : FB_BLOCKS;
+}
+
+extern "C" int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* scale, const float* shift,
+                                    const float* mean, const float* invstd, const float* coef, const void* yp,
+                                    const float* pscale, const float* pshift, const float* pmean, const float* pinvstd,
+                                    const void* wd, int kpad, int batch, int H, int W, void* dx, float* slab,
+                                    float* partials, sd_stream s) {
+    SD_REQUIRE(sd_conv3x3_bwd_fused_ok(32, 32, H, W) == 1 && batch > 0,
+               "sd_conv3x3_bwd_fused: 32 -> 32 channels, H %% 4 == 0, W %% 32 == 0 (got %dx%d)", H, W);
+    SD_REQUIRE(da && y && scale && shift && mean && invstd && coef && yp && pscale && pshift && pmean && pinvstd && wd &&
+                   dx && slab && partials && kpad >= 288,
+               "sd_conv3x3_bwd_fused: bad args");
+    BwdArgs p;
+    p.da = (const __bf16*)da;
+    p.y = (const __bf16*)y;
+    p.yp = (const __bf16*)yp;
+    p.sc = scale;
+    p.sh = shift;
+    p.mu = mean;
+    p.is = invstd;
+    p.coef = coef;
+    p.psc = pscale;
+    p.psh = pshift;
+    p.pmu = pmean;
+    p.pis = pinvstd;
+    p.wd = (const __bf16*)wd;
+    p.kpad = kpad;
+    p.B = batch;
+    p.H = H;
+    p.W = W;
+    p.tiles_x = W / FB_TW;
+    p.tiles_y = H / FB_TH;
+    const long long nt = (long long)batch * p.tiles_x * p.tiles_y;
+    SD_REQUIRE(nt < (1LL << 30), "sd_conv3x3_bwd_fused: too many tiles");
+    p.ntiles = (int)nt;
+    const int blocks = sd_conv3x3_bwd_fused_splits(batch, H, W);
+    p.tps = (int)((nt + blocks - 1) / blocks);
+    p.dx = (__bf16*)dx;
+    p.slab = slab;
+    p.part = reinterpret_cast<float2*>(partials);
+    hipLaunchKernelGGL(k_bwd_fused32, dim3(blocks), dim3(512), 0, to_stream(s), p);
+    return sd_check_launch("sd_conv3x3_bwd_fused");
+}

@@ -14,6 +14,7 @@
 // Tile shapes are runtime (8x32 at 240x320, 6x40 at 60x80, a whole 15x20 image ...): pixels of a
 // tile are flattened into 32-pixel MFMA rows / k-steps and each lane carries its pixel's halo offset.
 #include "common.h"
+#include "halo_util.h"
 
 namespace {
 
@@ -138,20 +139,6 @@ __device__ __forceinline__ uint4 halo_finish_pk(const HaloCol& hc, bool ok, uint
     return ok ? v : make_uint4(0, 0, 0, 0);
 }
 
-// halo_finish_pk's transform on an explicit per-channel affine (8 channels: s0|s1 scales, h0|h1 shifts)
-__device__ __forceinline__ uint4 bnrelu_pk(uint4 raw, float4 s0, float4 s1, float4 h0, float4 h1) {
-    const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
-    const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    unsigned o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float lo = __builtin_fmaf(__uint_as_float(w[i] << 16), s[2 * i], h[2 * i]);
-        const float hi = __builtin_fmaf(__uint_as_float(w[i] & 0xffff0000u), s[2 * i + 1], h[2 * i + 1]);
-        asm("v_cvt_pk_bf16_f32 %0, %1, %2\n\tv_pk_max_i16 %0, %0, 0" : "=v"(o[i]) : "v"(lo), "v"(hi));
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
 
 // Partner value for the BN-statistics reduce-scatter level o (16, 8, 4, 2, 1) within each 32-lane
 // half: lanes l and partner(l) differ in bit o and agree above it, which is all the reduce-scatter
@@ -243,7 +230,6 @@ struct HFwdArgs {
 #ifndef HC_VR
 #define HC_VR 1
 #endif
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 // BN statistics of one stored 16-B piece (8 bf16 channels; a pixel outside the tile adds zeros): channel pair q's
 // (sum, sum) in own[4q + {0,1}] and (sumsq, sumsq) in own[4q + {2,3}], so each pair is one v_pk_add_f32 and one
 // v_pk_fma_f32
@@ -259,31 +245,6 @@ __device__ __forceinline__ void stats_add(float* own, const uint4 v, const bool 
         own[4 * q + 1] = sm.y;
         own[4 * q + 2] = sq.x;
         own[4 * q + 3] = sq.y;
-    }
-}
-// BNS: the BatchNorm constants of a channel pair, -mean*invstd folded for xhat = y*invstd + nmi
-struct BnsK {
-    f32x2 sc, sh, is, nmi;
-};
-// BatchNorm-backward sums of one stored 16-B piece of da (8 bf16 channels) and the y piece of the same pixel:
-// dz = da where y*scale+shift > 0 (a pixel outside the tile adds zeros), own[4q + {0,1}] += dz and
-// own[4q + {2,3}] += dz*xhat for channel pair q, in packed fp32 pairs
-__device__ __forceinline__ void bns_add(float* own, const uint4 v, const uint4 yv, const bool live, const BnsK* bk) {
-    const unsigned wv[4] = {v.x, v.y, v.z, v.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const f32x2 d = {__uint_as_float(wv[q] << 16), __uint_as_float(wv[q] & 0xffff0000u)};
-        const f32x2 yy = {__uint_as_float(yw[q] << 16), __uint_as_float(yw[q] & 0xffff0000u)};
-        const f32x2 z = __builtin_elementwise_fma(yy, bk[q].sc, bk[q].sh);
-        const f32x2 xh = __builtin_elementwise_fma(yy, bk[q].is, bk[q].nmi);
-        const f32x2 dz = {(live & (z.x > 0.f)) ? d.x : 0.f, (live & (z.y > 0.f)) ? d.y : 0.f};
-        f32x2 sm = {own[4 * q], own[4 * q + 1]}, sx = {own[4 * q + 2], own[4 * q + 3]};
-        sm += dz;
-        sx = __builtin_elementwise_fma(dz, xh, sx);
-        own[4 * q] = sm.x;
-        own[4 * q + 1] = sm.y;
-        own[4 * q + 2] = sx.x;
-        own[4 * q + 3] = sx.y;
     }
 }
 template <bool B> struct BoolC { static constexpr bool v = B; };  // a compile-time flag passed to a generic lambda
@@ -1486,43 +1447,7 @@ __device__ __forceinline__ int wg_piece(int item) { return (item & 1) + ((item >
 constexpr int HP_PER_THREAD = HMAX * (CK / 8) / 256;  // wgrad halo pieces per thread (6)
 constexpr int WG_MAXPX = 256;   // pixels per wgrad tile (8 k-steps)
 
-// ds_read_b64_tr_b16 pair: rows r and r+8 (per-lane row addresses), 4 columns at col0+4*(i&3)
-__device__ __forceinline__ bf16x8 tr_pair(const __bf16* a0, const __bf16* a1) {
-    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
-    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
-    bf16x8 r;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        r[t] = lo[t];
-        r[t + 4] = hi[t];
-    }
-    return r;
-}
 
-// dy for 8 channels from the raw bf16 pieces (da, y): the BatchNorm-backward apply of k_bn_bwd_apply,
-// dy = k0*(dz - k1 - xhat*k2), dz = da where z = y*scale+shift > 0 (the forward ReLU mask, recomputed as
-// k_bn_bwd_apply does), xhat = (y-mean)*invstd, written in terms of z (which the mask needs anyway) with
-// k0 = scale: dy = scale*dz + Bz*z + Cz, Bz = -invstd*k2, Cz = invstd*k2*shift + scale*(mean*invstd*k2 - k1)
-__device__ __forceinline__ uint4 bn_bwd_pk(uint4 da, uint4 y, const float* sc, const float* sh, const float* Bz,
-                                           const float* Cz) {
-    const unsigned dw[4] = {da.x, da.y, da.z, da.w}, yw[4] = {y.x, y.y, y.z, y.w};
-    unsigned o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float r[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int c = 2 * i + h;
-            const float yv = __uint_as_float(h ? yw[i] & 0xffff0000u : yw[i] << 16);
-            const float dv = __uint_as_float(h ? dw[i] & 0xffff0000u : dw[i] << 16);
-            const float z = __builtin_fmaf(yv, sc[c], sh[c]);
-            const float t = __builtin_fmaf(Bz[c], z, Cz[c]);
-            r[h] = z > 0.f ? __builtin_fmaf(sc[c], dv, t) : t;
-        }
-        asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(o[i]) : "v"(r[0]), "v"(r[1]));
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
 
 template <int COUT, bool BNB>  // BNB: BatchNorm-backward apply in the dy staging (no dy written: enc1.0 has no dgrad)
 __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // two blocks per CU (LDS: 63-80 KB)

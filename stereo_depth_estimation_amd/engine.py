@@ -227,6 +227,9 @@ class UNetEngine:
         # bf16 training: the BatchNorm-backward sums of a block's conv0 from its conv1 dgrad epilogue
         # (sd_conv_gemm_bnsum; SD_BNSUM_FUSE=0: sd_bn_bwd_reduce pass)
         self.bnsum_fuse = os.environ.get("SD_BNSUM_FUSE", "1") != "0"
+        # bf16 training: the whole backward of the full-resolution 32 -> 32 conv1 layers (enc1.1, dec1.1) in one pass
+        # (sd_conv3x3_bwd_fused: dy stays in LDS; SD_BWD_FUSE=0: weight gradient + dgrad launches)
+        self.bwd_fuse = os.environ.get("SD_BWD_FUSE", "1") != "0"
         self._bnsum_rows: dict[str, int] = {}
         # training: the split-K slab reduce of every weight gradient on a second stream (SD_SIDE_REDUCE=1), so it
         # overlaps the next layer's kernels instead of adding a kernel boundary to the critical path; 2: the
@@ -420,7 +423,7 @@ class UNetEngine:
                 t["dy:" + cl.name] = act(lv, cl.cout)
                 t["coef:" + cl.name] = torch.empty(cl.cout, 3, dtype=f32, device=dev)
                 max_chan = max(max_chan, L.call("sd_chan_reduce_rows", P, cl.cout) * cl.cout * 2)
-                sp = L.call("sd_wgrad_splits", dt, B, H >> lv, W >> lv, cl.cout, 9 * cl.cin_pad)
+                sp = self._conv_splits(cl, B, H, W)
                 max_slab = max(max_slab, sp * cl.cout * 9 * cl.cin_pad)
             for u in self.ups.values():
                 lv = u.level
@@ -447,8 +450,7 @@ class UNetEngine:
                 ws.slab_off = {}
                 tot = 0
                 for cl in self.convs.values():
-                    lv = cl.level
-                    sp = L.call("sd_wgrad_splits", dt, B, H >> lv, W >> lv, cl.cout, 9 * cl.cin_pad)
+                    sp = self._conv_splits(cl, B, H, W)
                     ws.slab_off[cl.name] = tot
                     tot += _r16(sp * cl.cout * 9 * cl.cin_pad)
                 for u in self.ups.values():
@@ -465,6 +467,21 @@ class UNetEngine:
             t["heads_part"] = torch.empty(L.call("sd_heads_rows", P0) * (2 * self.c1 + 7), dtype=f32, device=dev)
         self.ws = ws
         return ws
+
+    def _bwd_fused(self, cl: ConvL, H: int, W: int) -> bool:
+        """Whether conv `cl`'s backward runs as one sd_conv3x3_bwd_fused pass (bf16 training, a 32 -> 32 conv1 whose
+        input is its block's conv0 output, at a tiling the kernel takes: enc1.1 and dec1.1 at full resolution)."""
+        return (self.bwd_fuse and self.sd_dtype == L.SD_BF16 and cl.idx == 1 and cl.cout == 32 and cl.cin == 32
+                and self.bnsum_fuse and L.call("sd_conv3x3_bwd_fused_ok", cl.cout, cl.cin, H >> cl.level,
+                                               W >> cl.level) == 1)
+
+    def _conv_splits(self, cl: ConvL, B: int, H: int, W: int) -> int:
+        """Split-K slabs of conv `cl`'s weight gradient (its slab region holds the larger of the two kernels')."""
+        lv = cl.level
+        sp = L.call("sd_wgrad_splits", self.sd_dtype, B, H >> lv, W >> lv, cl.cout, 9 * cl.cin_pad)
+        if self._bwd_fused(cl, H, W):
+            sp = max(sp, L.call("sd_conv3x3_bwd_fused_splits", B, H >> lv, W >> lv))
+        return sp
 
     # ------------------------------------------------------------------ forward
     def _bn(self, cl: ConvL):
@@ -1029,6 +1046,23 @@ class UNetEngine:
     def _conv_bwd(self, cl: ConvL, need_dgrad: bool, fused_rows: int = 0):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         Hl, Wl = ws.H >> cl.level, ws.W >> cl.level
+        if need_dgrad and self._bwd_fused(cl, ws.H, ws.W):
+            # one pass: dy = BatchNorm-backward(da, y) staged in LDS, the weight gradient's split-K slabs, the dgrad
+            # into da of conv0 and conv0's BatchNorm-backward sums (4 full-resolution tensor passes instead of 7)
+            self._bn_bwd(cl, fused_rows, apply=False)
+            c0 = self.convs[cl.blk + ".0"]
+            sp = L.call("sd_conv3x3_bwd_fused_splits", ws.B, Hl, Wl)
+            args = (t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), t["scale:" + cl.name].data_ptr(),
+                    t["shift:" + cl.name].data_ptr(), t["mean:" + cl.name].data_ptr(),
+                    t["invstd:" + cl.name].data_ptr(), t["coef:" + cl.name].data_ptr(), t["y:" + c0.name].data_ptr(),
+                    t["scale:" + c0.name].data_ptr(), t["shift:" + c0.name].data_ptr(),
+                    t["mean:" + c0.name].data_ptr(), t["invstd:" + c0.name].data_ptr(), self._wp(cl.off_d),
+                    cl.kpad_d, ws.B, Hl, Wl, t["da:" + c0.name].data_ptr())
+            self._wgrad_slabs(lambda slab, st: L.call("sd_conv3x3_bwd_fused", *args, slab, t["chan"].data_ptr(), st),
+                              sp, cl.cout, 9 * cl.cin_pad, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key],
+                              gemm_may_side=False, key=cl.name)
+            self._bnsum_rows[c0.name] = sp
+            return
         dy = t["dy:" + cl.name]
         a = L.make_src(dy, cl.cout, Hl, Wl, taps=1)
         b = self._src_fwd(cl)

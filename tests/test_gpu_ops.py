@@ -910,3 +910,59 @@ def test_conv3x3_raw_source_dma_loaders_bit_identical(monkeypatch, B, H, W, c0, 
     assert torch.equal(a0, b0) and torch.equal(a1, b1)
     got = _from_nhwc(o1[lib.SD_EPI_STORE][0], B, H, W, co)
     assert float((got - ref).abs().max()) <= _tol(ref, "bf16")
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 16, 64), (1, 8, 32), (3, 12, 96)])
+def test_conv3x3_bwd_fused_matches_reference(B, H, W):
+    """sd_conv3x3_bwd_fused (enc1.1 / dec1.1 backward in one pass) against fp64 PyTorch on the same bf16 operands:
+    dy = BatchNorm-backward(da, y) (the kernel stages it as bf16), dW = conv2d_weight(x, dy), x = relu(bn_prev(y_prev))
+    (bf16), dx = conv2d_input(dy, W) (stored bf16), and the previous layer's BatchNorm-backward sums over (dx, y_prev).
+    Bounds: dW 1e-3 of max (fp32 sums of bf16 products), dx one bf16 rounding (2^-7 relative + 1e-3 of max), sums 1e-2
+    of their scale (they are taken over the bf16-rounded dx)."""
+    lib = L()
+    torch.manual_seed(31)
+    C = 32
+    bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    da, y, yp = bf(torch.randn(B, C, H, W)), bf(torch.randn(B, C, H, W)), bf(torch.randn(B, C, H, W))
+    sc, sh = torch.rand(C).double() + 0.5, torch.randn(C).double() * 0.3
+    sc[::5] *= -1
+    mu, is_ = torch.randn(C).double() * 0.2, torch.rand(C).double() + 0.5
+    coef = torch.randn(C, 3).double() * 0.1
+    psc, psh = torch.rand(C).double() + 0.5, torch.randn(C).double() * 0.3
+    pmu, pis = torch.randn(C).double() * 0.2, torch.rand(C).double() + 0.5
+    w = (torch.randn(C, C, 3, 3) / 17.0).to(torch.bfloat16).double()
+    v = lambda t: t[None, :, None, None]  # noqa: E731
+    # reference
+    z = y * v(sc) + v(sh)
+    dz = torch.where(z > 0, da, torch.zeros_like(da))
+    dy = v(sc) * (dz - v(coef[:, 1]) - v(coef[:, 2]) * (y - v(mu)) * v(is_))
+    dy = bf(dy.float())
+    x = bf(torch.relu(yp * v(psc) + v(psh)).float())
+    dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, padding=1)
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=1)
+    # kernel
+    f32 = lambda t: t.float().contiguous().to(DEV)  # noqa: E731
+    wp, kpad = _pack3(w.float(), C, True, "bf16")
+    sp = lib.call("sd_conv3x3_bwd_fused_splits", B, H, W)
+    assert lib.call("sd_conv3x3_bwd_fused_ok", C, C, H, W) == 1
+    slab = torch.full((sp * C * 9 * C,), float("nan"), device=DEV)
+    part = torch.full((sp, C, 2), float("nan"), device=DEV)
+    dx = torch.full((B * H * W, C), float("nan"), dtype=torch.bfloat16, device=DEV)
+    tens = [_nhwc(t.float(), "bf16") for t in (da, y, yp)]
+    prm = [f32(t) for t in (sc, sh, mu, is_, coef, psc, psh, pmu, pis)]
+    lib.call("sd_conv3x3_bwd_fused", tens[0].data_ptr(), tens[1].data_ptr(), *[t.data_ptr() for t in prm[:5]],
+             tens[2].data_ptr(), *[t.data_ptr() for t in prm[5:]], wp.data_ptr(), kpad, B, H, W, dx.data_ptr(),
+             slab.data_ptr(), part.data_ptr(), lib.stream_handle())
+    dw = torch.empty(C, C, 3, 3, device=DEV)
+    lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, C, 9 * C, lib.SD_W_CONV3, C, dw.data_ptr(), lib.stream_handle())
+    torch.cuda.synchronize()
+    dw = dw.double().cpu()
+    assert float((dw - dw_ref).abs().max()) <= 1e-3 * float(dw_ref.abs().max())
+    got = _from_nhwc(dx, B, H, W, C).double()
+    assert float(((got - dx_ref).abs() - 2.0 ** -7 * dx_ref.abs()).max()) <= 1e-3 * float(dx_ref.abs().max())
+    # the previous layer's BatchNorm-backward sums over the stored (bf16) dx
+    dzp = torch.where(yp * v(psc) + v(psh) > 0, got, torch.zeros_like(got))
+    xh = (yp - v(pmu)) * v(pis)
+    s_ref = torch.stack([dzp.sum((0, 2, 3)), (dzp * xh).sum((0, 2, 3))], 1)
+    s_got = part.double().sum(0).cpu()
+    assert float((s_got - s_ref).abs().max()) <= 1e-2 * (1 + float(s_ref.abs().max()))
