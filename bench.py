@@ -16,7 +16,8 @@ warmup steps, barrier + synchronize, K steps, barrier + synchronize, max over ra
 `roofline`: the dominant GEMM kernel instance (largest summed time), timed live with HIP
 events around each of its launches inside the timed region; achieved = algorithmic FLOPs
 (2*M*N*K with real, unpadded channels) per launch / mean launch duration; peak = 2500
-TFLOP/s dense bf16 (MI355X_MICROARCH.md). `traffic` = that kernel's HBM bytes per launch from
+TFLOP/s dense bf16 (MI355X_MICROARCH.md). A kernel below the ridge (FLOP per byte < 2500/8) is priced in
+bytes instead: algorithmic bytes per launch / mean launch duration against 8000 GB/s. `traffic` = that kernel's HBM bytes per launch from
 the committed rocprofv3 PMC summary of this same command (profiles/pmc_traffic.json, made by
 tools/pmc_traffic.py: 1024*(2*FETCH_SIZE + WRITE_SIZE), the guide's gfx950 corrections).
 `cpu_baseline`: the oracle's PyTorch-CPU fp32 restatement of the reference train step (B=2,
@@ -87,6 +88,9 @@ class GemmTimer:
 
     def _flops_and_name(self, name, args):
         L, eng = self.L, self.eng
+        if name == "sd_conv3x3_bwd_fused":  # weight gradient + dgrad of a 32 -> 32 full-resolution conv, one pass
+            B, H, W = args[14:17]
+            return 2.0 * 2.0 * B * H * W * 32 * 9 * 32, "k_bwd_fused32"
         xin = eng.ws.t["xin"].data_ptr()
         if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             dt, src, B, H, W, _, N = args[:7]
@@ -108,7 +112,8 @@ class GemmTimer:
         return 2.0 * B * H * W * M * n_real, L.kernel_name("sd_wgrad_kernel_name", dt, a, sb, M, N)
 
     def __call__(self, name, args, phase):
-        if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd"):
+        if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd",
+                        "sd_conv3x3_bwd_fused"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
         ev.record(self._stream(args[-1]))  # the launch stream (SD_SIDE_REDUCE=2 puts some GEMMs on a second one)
@@ -120,6 +125,8 @@ class GemmTimer:
         else:
             start, flops, kname = self.cur
             nbytes = self._min_bytes(args) if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum") else 0.0
+            if name == "sd_conv3x3_bwd_fused":  # da, y, y_prev read, dx written once (bf16, 32 channels)
+                nbytes = 4.0 * args[14] * args[15] * args[16] * 32 * 2
             self.pending.append((kname, flops, start, ev, name, self._shape(name, args), nbytes))
             if name == "sd_conv_gemm" and self._last_phase == "fwd":
                 # forward order (model.py:79-104): the first 10 3x3 convs are enc1..enc4, bottleneck
@@ -173,6 +180,8 @@ class GemmTimer:
 
     @staticmethod
     def _shape(name, args):
+        if name == "sd_conv3x3_bwd_fused":
+            return f"bwd_fused P={args[14] * args[15] * args[16]} C=32"
         if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             s = args[1]
             return f"fwd M={args[2] * args[3] * args[4]} N={args[6]} K={s.taps}x{s.chans[0] + s.chans[1]}"
@@ -570,15 +579,21 @@ def main():
         alg = top.get("alg_bytes_per_launch")
         ai_alg = top["flops_per_launch"] / alg if alg else None
         ai_b = ai if ai is not None else ai_alg
+        bound = ("mfma" if ai_b >= peak * 1e12 / 8e12 else "hbm") if ai_b is not None else None
+        if bound == "hbm":  # priced in bytes: algorithmic bytes per launch / launch time against 8 TB/s
+            ach, pk, unit = alg / (top["avg_us"] * 1e-6) / 1e9, 8000.0, "GB/s"
+        else:
+            ach, pk, unit = top["tflops"], peak, "TFLOP/s"
         result["roofline"] = {
-            "bound": ("mfma" if ai_b >= peak * 1e12 / 8e12 else "hbm") if ai_b is not None else None,
+            "bound": bound,
             "alg_bytes_per_launch": alg,
             "flop_per_alg_byte": round(ai_alg, 1) if ai_alg else None,
             "kernel": top["kernel"],
-            "achieved": round(top["tflops"], 2),
-            "peak": peak,
-            "unit": "TFLOP/s",
-            "frac": round(top["tflops"] / peak, 4),
+            "achieved": round(ach, 2),
+            "peak": pk,
+            "unit": unit,
+            "frac": round(ach / pk, 4),
+            "tflops": round(top["tflops"], 2),
             "traffic": traffic,
             "traffic_source": tsrc,
             "flop_per_byte": round(ai, 1) if ai else None,

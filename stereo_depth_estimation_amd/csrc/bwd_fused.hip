@@ -9,13 +9,13 @@
 // wrote dy) and the BatchNorm-sums dgrad (k_halo_conv<1, 4, 32, ..., BNS>: read dy, y_prev, wrote dx): per layer
 // 4 full-resolution tensor passes (da, y, y_prev in; dx out) instead of 7.
 //
-// One 512-thread block per CU, persistent over a contiguous range of 4x32-pixel tiles (its split-K range):
-//   waves 4-7 (loaders): per tile, the 6x34 halo of (da, y) -> dy and of y_prev -> x (BN + ReLU), through registers
-//                        (two tiles in flight) into an LDS double buffer, plus the raw y_prev of the tile's interior
-//                        (for the sums);
+// One 512-thread block per CU, persistent over a contiguous range of 8x16-pixel tiles (its split-K range):
+//   waves 4-7 (loaders): per tile, the 10x18 halo of (da, y) -> dy and of y_prev -> x (BN + ReLU), through registers
+//                        (two tiles in flight) into an LDS double buffer;
 //   waves 0-3 (MFMA)   : weight gradient (16 co x 16 ci per wave, v_mfma_f32_16x16x32_bf16 on transposed fragments,
-//                        k = tile pixels) and dgrad (one 32-pixel tile row per wave, all 32 ci, 32x32x16 MFMAs over
-//                        9 taps x 32 dy channels with the dgrad weights resident in LDS), then the dgrad epilogue.
+//                        k = tile pixels) and dgrad (32 tile pixels = two rows per wave, all 32 ci, 32x32x16 MFMAs over
+//                        9 taps x 32 dy channels with the dgrad weights resident in LDS), then the dgrad epilogue
+//                        (the sums read the raw y_prev from L2).
 #include <stdio.h>
 
 #include "halo_util.h"
@@ -24,17 +24,27 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int FB_TH = 4, FB_TW = 32;               // output tile
+constexpr int FB_TH = 8, FB_TW = 16;               // output tile: 4 units of 32 pixels (2 rows each)
 constexpr int FB_HW = FB_TW + 2, FB_HH = FB_TH + 2;  // halo width / rows
-constexpr int FB_HPX = FB_HW * FB_HH;              // 204 halo pixels
-constexpr int FB_NI = 4;                           // loader items per thread (4 x 256 >= 204 pixels x 4 pieces)
+constexpr int FB_HPX = FB_HW * FB_HH;              // 180 halo pixels
+constexpr int FB_NI = (FB_HPX * 4 + 255) / 256;    // loader items per thread (3 x 256 >= 180 pixels x 4 pieces)
+constexpr int FB_HSL = (FB_NI * 256 / 32) * 8;     // halo pixel slots (items past the halo land in slots >= FB_HPX)
+static_assert(FB_TH * FB_TW == 128 && FB_TW % 16 == 0, "4 MFMA waves x 32 pixels; tr_pair rows p, p + 8 in one row");
 constexpr int FB_DL = 40;                          // dy halo pixel pitch (80 B: odd 16-B slot count, b128 reads)
 constexpr int FB_XL = 48;                          // x halo pixel pitch (96 B: conflict-free transposed reads)
-constexpr int FB_SL = 40;                          // raw y_prev stash pitch
 constexpr int FB_WL = 9 * 32 + 8;                  // dgrad weight row (592 B, odd slot count)
-constexpr int FB_DYH = 256 * FB_DL, FB_XH = 256 * FB_XL, FB_ST = FB_TH * FB_TW * FB_SL;
-constexpr int FB_BUF = FB_DYH + FB_XH + FB_ST;     // elements per LDS buffer
+constexpr int FB_DYH = FB_HSL * FB_DL, FB_XH = FB_HSL * FB_XL;
+constexpr int FB_BUF = FB_DYH + FB_XH;             // elements per LDS buffer
 constexpr int FB_BLOCKS = 256;                     // one per CU
+#ifndef FB_EXP
+#define FB_EXP 0  // timing-only builds (results wrong): 1 no loader transform, 2 no wgrad, 4 no dgrad, 8 no dgrad
+                  // epilogue, 16 no loads after the first two tiles, 32 per-wave phase cycle counters (sd_debug_buffer)
+#endif
+constexpr bool FB_DG = (FB_EXP & 32) != 0;
+__device__ __forceinline__ unsigned long long fb_clk() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memtime();
+}
 
 struct BwdArgs {
     const __bf16 *da, *y, *yp;                        // [B*H*W][32]
@@ -46,12 +56,25 @@ struct BwdArgs {
     __bf16* dx;                                       // [B*H*W][32]
     float* slab;                                      // [blocks][32 co][288], k = tap*32 + ci
     float2* part;                                     // [blocks][32] (sum dz, sum dz*xhat) of the previous layer
+    unsigned long long* dbg;                          // timing build only: [block][wave][8] phase cycles
 };
+
+template <bool B> struct BoolC { static constexpr bool v = B; };
 
 template <int PPX>
 __device__ __forceinline__ int fb_pixel(int item) { return (item / (8 * PPX)) * 8 + (item & 7); }
 template <int PPX>
 __device__ __forceinline__ int fb_piece(int item) { return (item >> 3) % PPX; }
+
+// tile index -> (column strip tx, tile row ty, image b), ty fastest: a block walks down a 32-pixel column strip, so
+// the two halo rows a tile shares with the one above were loaded one tile earlier and are L2 hits (row-major order
+// re-fetched them from beyond L2 one tile row = 10 tiles later: 1.5x the algorithmic reads, PMC)
+__device__ __forceinline__ void fb_tile(const BwdArgs& p, int tl, int& tx, int& ty, int& b) {
+    ty = tl % p.tiles_y;
+    const int r = tl / p.tiles_y;
+    tx = r % p.tiles_x;
+    b = r / p.tiles_x;
+}
 
 __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * FB_BUF];
@@ -95,27 +118,32 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
         const float4 s1 = *reinterpret_cast<const float4*>(p.psc + piece * 8 + 4);
         const float4 t0 = *reinterpret_cast<const float4*>(p.psh + piece * 8);
         const float4 t1 = *reinterpret_cast<const float4*>(p.psh + piece * 8 + 4);
-        // halo geometry of the items: (row << 8 | col), ~0 past the halo; interior stash slot or -1
+        // halo geometry of the items: (row << 8 | col), ~0 past the halo
         unsigned geo[FB_NI];
-        int stash[FB_NI];
 #pragma unroll
         for (int i = 0; i < FB_NI; ++i) {
             const int px = fb_pixel<4>(ltid + 256 * i);
             const int hy = px / FB_HW, hx = px - hy * FB_HW;
             geo[i] = px < FB_HPX ? (unsigned)(hy << 8 | hx) : 0xffffffffu;
-            const bool in = px < FB_HPX && hy >= 1 && hy <= FB_TH && hx >= 1 && hx <= FB_TW;
-            stash[i] = in ? ((hy - 1) * FB_TW + hx - 1) * FB_SL + piece * 8 : -1;
         }
+        // items FB_HPX * 4.. are past the halo: a loader wave whose first item of the last slot is past it skips that
+        // slot (wave-uniform)
+        const bool w3 = (ltid & ~63) + 256 * (FB_NI - 1) < FB_HPX * 4;
+        unsigned need = 0;
+#pragma unroll
+        for (int i = 0; i < FB_NI; ++i) need |= (unsigned)(geo[i] != 0xffffffffu) << i;
         struct Set {
             uint4 a[FB_NI], y[FB_NI], x[FB_NI];
             unsigned m;  // bit i: item i inside the image
+            bool edge;   // wave-uniform: some halo item of the wave is padding (outside the image or the range)
         };
         Set sa, sb;
         auto load = [&](Set& q, int tile) __attribute__((always_inline)) {
+            if ((FB_EXP & 16) && tile >= t_begin + 2) return;
             const bool live = tile < t_begin + ntile;
             const int tl = live ? tile : t_begin;
-            const int tx = tl % p.tiles_x, r = tl / p.tiles_x;
-            const int ty = r % p.tiles_y, b = r / p.tiles_y;
+            int tx, ty, b;
+            fb_tile(p, tl, tx, ty, b);
             const int h0 = ty * FB_TH - 1, w0 = tx * FB_TW - 1;
             const size_t img = (size_t)b * hw * 32;
             const __amdgpu_buffer_rsrc_t ra =
@@ -127,6 +155,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             unsigned m = 0;
 #pragma unroll
             for (int i = 0; i < FB_NI; ++i) {
+                if (i == FB_NI - 1 && !w3) break;
                 const int h = h0 + (int)(geo[i] >> 8), w = w0 + (int)(geo[i] & 0xffu);
                 const bool ok = live & (geo[i] != 0xffffffffu) & (h >= 0) & (h < p.H) & (w >= 0) & (w < p.W);
                 m |= (unsigned)ok << i;
@@ -139,23 +168,31 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
                 q.x[i] = make_uint4(vp[0], vp[1], vp[2], vp[3]);
             }
             q.m = m;
+            q.edge = __builtin_amdgcn_ballot_w64(m != (w3 ? need : need & ((1u << (FB_NI - 1)) - 1))) != 0;
         };
         auto store = [&](Set& q, int buf) __attribute__((always_inline)) {
             __bf16* dyh = smem + buf * FB_BUF;
             __bf16* xh = dyh + FB_DYH;
-            __bf16* st = xh + FB_XH;
+            auto put = [&](auto SEL) __attribute__((always_inline)) {
 #pragma unroll
-            for (int i = 0; i < FB_NI; ++i) {
-                const bool ok = (q.m >> i) & 1u;
-                const int px = fb_pixel<4>(ltid + 256 * i);  // < 256: inside the regions (items past the halo unused)
-                uint4 d = bn_bwd_pk(q.a[i], q.y[i], ksc, ksh, kB, kC);
-                d = ok ? d : make_uint4(0, 0, 0, 0);  // the dgrad's zero padding, and dy past the image
-                uint4 x = bnrelu_pk(q.x[i], s0, s1, t0, t1);
-                x = ok ? x : make_uint4(0, 0, 0, 0);
-                *reinterpret_cast<uint4*>(dyh + px * FB_DL + piece * 8) = d;
-                *reinterpret_cast<uint4*>(xh + px * FB_XL + piece * 8) = x;
-                if (stash[i] >= 0) *reinterpret_cast<uint4*>(st + stash[i]) = q.x[i];  // raw y_prev (0 past the image)
-            }
+                for (int i = 0; i < FB_NI; ++i) {
+                    if (i == FB_NI - 1 && !w3) break;
+                    const bool ok = (q.m >> i) & 1u;
+                    const int px = fb_pixel<4>(ltid + 256 * i);  // < FB_HSL (items past the halo unused)
+                    uint4 d = (FB_EXP & 1) ? q.a[i] : bn_bwd_pk(q.a[i], q.y[i], ksc, ksh, kB, kC);
+                    uint4 x = (FB_EXP & 1) ? q.x[i] : bnrelu_pk(q.x[i], s0, s1, t0, t1);
+                    if constexpr (decltype(SEL)::v) {  // the dgrad's zero padding, and dy past the image
+                        d = ok ? d : make_uint4(0, 0, 0, 0);
+                        x = ok ? x : make_uint4(0, 0, 0, 0);
+                    }
+                    *reinterpret_cast<uint4*>(dyh + px * FB_DL + piece * 8) = d;
+                    *reinterpret_cast<uint4*>(xh + px * FB_XL + piece * 8) = x;
+                }
+            };
+            if (q.edge)
+                put(BoolC<true>{});
+            else
+                put(BoolC<false>{});
         };
         load(sa, t_begin);
         __builtin_amdgcn_sched_barrier(0);
@@ -163,13 +200,45 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
         __syncthreads();  // the resident weights (the MFMA waves meet it before their first tile)
         // an even number of iterations (no exit between the two register sets); an odd count's last one stores a
         // tile past the range into the buffer the MFMA waves no longer read
+        unsigned long long tc[5] = {0, 0, 0, 0, 0}, tm0 = 0, t_all = FB_DG ? fb_clk() : 0;
+        auto stamp = [&](int k) __attribute__((always_inline)) {
+            if (FB_DG) {
+                const unsigned long long t1 = fb_clk();
+                tc[k] += t1 - tm0;
+                tm0 = t1;
+            }
+        };
         for (int i = 0; i < ntile; i += 2) {
+            if (FB_DG) {
+                tm0 = fb_clk();
+                asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // this set's loads (9-12 of the other set stay)
+                stamp(3);
+            }
             store(sa, 0);
+            stamp(0);
             load(sa, t_begin + i + 2);
+            stamp(1);
             __syncthreads();
+            stamp(2);
+            if (FB_DG) {
+                asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+                stamp(3);
+            }
             store(sb, 1);
+            stamp(0);
             load(sb, t_begin + i + 3);
+            stamp(1);
             __syncthreads();
+            stamp(2);
+        }
+        if (FB_DG && p.dbg && lane == 0) {
+            unsigned long long* d = p.dbg + ((size_t)bid * 8 + 4 + wid) * 8;
+            d[0] = tc[0];
+            d[1] = tc[1];
+            d[2] = tc[2];
+            d[3] = tc[3];
+            d[4] = fb_clk() - t_all;
+            d[5] = ntile;
         }
         __syncthreads();  // the statistics reduction (MFMA waves)
         return;
@@ -211,35 +280,68 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
     for (int j = 0; j < 16; ++j) own[j] = 0.f;
     __bf16* const scw = scr + wid * 32 * 32;
     auto swz = [](int j, int px) { return j ^ ((px >> 1) & 3); };
+    unsigned long long tc[4] = {0, 0, 0, 0}, t0 = 0, t_all = FB_DG ? fb_clk() : 0;
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+        if (FB_DG) {
+            const unsigned long long t1 = fb_clk();
+            tc[k] += t1 - t0;
+            t0 = t1;
+        }
+    };
     for (int it = 0; it < ntile; ++it) {
+        if (FB_DG) t0 = fb_clk();
         __syncthreads();  // tile it is in buffer it & 1
+        stamp(0);
         const __bf16* dyh = smem + (it & 1) * FB_BUF;
         const __bf16* xh = dyh + FB_DYH;
-        const __bf16* st = xh + FB_XH;
-        // ---- weight gradient: k = the tile's pixels, 4 k-steps of one 32-pixel tile row each
+        // the raw y_prev of this wave's epilogue pieces (the sums' xhat and ReLU mask), from L2 (the loaders fetched
+        // them two tiles ago), in flight through the MFMA phases
+        const int tl = t_begin + it;
+        int tx, ty, b;
+        fb_tile(p, tl, tx, ty, b);
+        const int h0 = ty * FB_TH, w0 = tx * FB_TW;
+        uint4 yv[2];
+        {
+            const __amdgpu_buffer_rsrc_t ryp = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(p.yp + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
 #pragma unroll
-        for (int ks = 0; ks < FB_TH; ++ks) {
-            const __bf16* a0 = dyh + ((ks + 1) * FB_HW + 1 + pc) * FB_DL + co0 + 4 * pp;  // dy^T of tile row ks
+            for (int rr = 0; rr < 2; ++rr) {
+                const int q = wid * 32 + rr * 16 + (lane >> 2), j = lane & 3;  // tile pixel q
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+                    ryp, (unsigned)((h0 + q / FB_TW) * p.W + w0 + q % FB_TW) * 64u + (unsigned)j * 16u, 0, 0);
+                yv[rr] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        // ---- weight gradient: k = the tile's pixels, 4 k-steps of 32 (tile pixels q = 32 ks + pc, + 8: one row)
+#pragma unroll
+        for (int ks = 0; ks < ((FB_EXP & 2) ? 0 : 4); ++ks) {
+            const int q = ks * 32 + pc, r = q / FB_TW, c = q % FB_TW;
+            const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + c) * FB_DL + co0 + 4 * pp;  // dy^T
             const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
             bf16x8 bf[9];
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                const __bf16* x0 = xh + ((ks + tap / 3) * FB_HW + tap % 3 + pc) * FB_XL + ci0 + 4 * pp;
+                const __bf16* x0 = xh + ((r + tap / 3) * FB_HW + tap % 3 + c) * FB_XL + ci0 + 4 * pp;
                 bf[tap] = tr_pair(x0, x0 + 8 * FB_XL);
             }
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap)
                 accw[tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[tap], accw[tap], 0, 0, 0);
         }
-        // ---- dgrad of tile row `wid`: C^T[ci][px] over 9 taps x 2 k-steps of 16 dy channels
+        if (FB_DG) {  // the weight gradient's MFMAs retired
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            stamp(1);
+        }
+        // ---- dgrad of tile pixels 32 wid ..: C^T[ci][px] over 9 taps x 2 k-steps of 16 dy channels
         f32x16 accd;
 #pragma unroll
         for (int r = 0; r < 16; ++r) accd[r] = 0.f;
         const int c8 = 8 * (lane >> 5);
         const __bf16* wrow = wds + (lane & 31) * FB_WL + c8;
-        const __bf16* drow = dyh + (wid * FB_HW + (lane & 31)) * FB_DL + c8;
+        const int qd = wid * 32 + (lane & 31);
+        const __bf16* drow = dyh + ((qd / FB_TW) * FB_HW + qd % FB_TW) * FB_DL + c8;
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
+        for (int tap = 0; tap < ((FB_EXP & 4) ? 0 : 9); ++tap) {
             const int toff = ((tap / 3) * FB_HW + tap % 3) * FB_DL;
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
@@ -248,10 +350,14 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
                 accd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, accd, 0, 0, 0);
             }
         }
+        if (FB_DG) {
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            stamp(2);
+        }
         // ---- dgrad epilogue: lanes l / l + 32 hold the 4-channel halves of each 8-channel group of pixel l & 31;
         // v_permlane32_swap pairs them into whole 16-B pieces, which go through the wave's scratch and leave as
         // pixel rows (16 pixels x 4 pieces per store instruction), with the previous layer's BatchNorm-backward sums
-        {
+        if (!(FB_EXP & 8)) {
             uint2 pk[4];
 #pragma unroll
             for (int g4 = 0; g4 < 4; ++g4) {
@@ -268,30 +374,38 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
                 *reinterpret_cast<uint4*>(scw + px * 32 + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
             }
             asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
-            const int tl = t_begin + it;
-            const int tx = tl % p.tiles_x, r = tl / p.tiles_x;
-            const int ty = r % p.tiles_y, b = r / p.tiles_y;
-            const int h = ty * FB_TH + wid, w0 = tx * FB_TW;
             const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.dx + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
-            uint4 vv[2], yv[2];
+            uint4 vv[2];
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
                 const int px = rr * 16 + (lane >> 2), j = lane & 3;
                 vv[rr] = *reinterpret_cast<const uint4*>(scw + px * 32 + swz(j, px) * 8);
-                yv[rr] = *reinterpret_cast<const uint4*>(st + (wid * FB_TW + px) * FB_SL + j * 8);
             }
             asm volatile("" ::: "memory");  // the next tile's scratch writes after these reads
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
-                const int px = rr * 16 + (lane >> 2), j = lane & 3;
-                const bool live = (h < p.H) & (w0 + px < p.W);
+                const int q = wid * 32 + rr * 16 + (lane >> 2), j = lane & 3;
+                const int h = h0 + q / FB_TW, w = w0 + q % FB_TW;
+                const bool live = (h < p.H) & (w < p.W);
                 bns_add(own, vv[rr], yv[rr], live, bk);
                 __attribute__((ext_vector_type(4))) unsigned data = {vv[rr].x, vv[rr].y, vv[rr].z, vv[rr].w};
-                const unsigned off = live ? (unsigned)(h * p.W + w0 + px) * 64u + (unsigned)j * 16u : 0x80000000u;
+                const unsigned off = live ? (unsigned)(h * p.W + w) * 64u + (unsigned)j * 16u : 0x80000000u;
                 __builtin_amdgcn_raw_buffer_store_b128(data, rd, off, 0, 2);
             }
+        } else if (accd[0] == 1.2345e-30f) {  // timing build: keep the dgrad MFMAs live
+            p.dx[lane] = (__bf16)accd[1];
         }
+        stamp(3);
+    }
+    if (FB_DG && p.dbg && lane == 0) {
+        unsigned long long* d = p.dbg + ((size_t)bid * 8 + wid) * 8;
+        d[0] = tc[0];
+        d[1] = tc[1];
+        d[2] = tc[2];
+        d[3] = tc[3];
+        d[4] = fb_clk() - t_all;
+        d[5] = ntile;
     }
     if (ntile & 1) __syncthreads();  // the loaders' last (even-count) iteration
 
@@ -326,6 +440,8 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
 
 }  // namespace
 
+unsigned long long* sd_debug_ptr();
+
 extern "C" int sd_conv3x3_bwd_fused_ok(int C, int Cx, int H, int W) {
     return C == 32 && Cx == 32 && H % FB_TH == 0 && W % FB_TW == 0 && W / FB_TW < 256 && (long long)H * W * 64 < (1LL << 31)
                ? 1
@@ -343,7 +459,7 @@ extern "C" int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* 
                                     const void* wd, int kpad, int batch, int H, int W, void* dx, float* slab,
                                     float* partials, sd_stream s) {
     SD_REQUIRE(sd_conv3x3_bwd_fused_ok(32, 32, H, W) == 1 && batch > 0,
-               "sd_conv3x3_bwd_fused: 32 -> 32 channels, H %% 4 == 0, W %% 32 == 0 (got %dx%d)", H, W);
+               "sd_conv3x3_bwd_fused: 32 -> 32 channels, H %% %d == 0, W %% %d == 0 (got %dx%d)", FB_TH, FB_TW, H, W);
     SD_REQUIRE(da && y && scale && shift && mean && invstd && coef && yp && pscale && pshift && pmean && pinvstd && wd &&
                    dx && slab && partials && kpad >= 288,
                "sd_conv3x3_bwd_fused: bad args");
@@ -375,6 +491,7 @@ extern "C" int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* 
     p.dx = (__bf16*)dx;
     p.slab = slab;
     p.part = reinterpret_cast<float2*>(partials);
+    p.dbg = FB_DG ? sd_debug_ptr() : nullptr;
     hipLaunchKernelGGL(k_bwd_fused32, dim3(blocks), dim3(512), 0, to_stream(s), p);
     return sd_check_launch("sd_conv3x3_bwd_fused");
 }

@@ -2128,6 +2128,7 @@ extern "C" int sd_debug_buffer(void* p) {
     g_wg_dbg = (unsigned long long*)p;
     return 0;
 }
+unsigned long long* sd_debug_ptr() { return g_wg_dbg; }  // the fused backward's timing build (bwd_fused.hip)
 
 bool sd_halo_fwd_shape(int N) { return N == 32 || N % 64 == 0; }
 bool sd_halo_fwd_ok(const sd_src& a, int N, int epi) {

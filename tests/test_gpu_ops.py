@@ -912,7 +912,7 @@ def test_conv3x3_raw_source_dma_loaders_bit_identical(monkeypatch, B, H, W, c0, 
     assert float((got - ref).abs().max()) <= _tol(ref, "bf16")
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 16, 64), (1, 8, 32), (3, 12, 96)])
+@pytest.mark.parametrize("B,H,W", [(2, 16, 64), (1, 8, 32), (3, 24, 48)])
 def test_conv3x3_bwd_fused_matches_reference(B, H, W):
     """sd_conv3x3_bwd_fused (enc1.1 / dec1.1 backward in one pass) against fp64 PyTorch on the same bf16 operands:
     dy = BatchNorm-backward(da, y) (the kernel stages it as bf16), dW = conv2d_weight(x, dy), x = relu(bn_prev(y_prev))

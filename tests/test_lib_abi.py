@@ -100,6 +100,12 @@ def test_planning_queries_are_host_only():
     assert L.call("sd_conv3x3_fp8_rows", 1, 45, 60, 512) == 12  # 4x60 tiles, 8 N-blocks
     assert L.kernel_name("sd_conv3x3_fp8_kernel_name", 64) == "k_halo_conv_fp8<2>"
     assert L.call("sd_chan_minmax_rows", 691200, 32) == 256
+    # fused full-resolution conv1 backward: 32 -> 32 channels on 8x16 tiles, one block per CU
+    assert L.call("sd_conv3x3_bwd_fused_ok", 32, 32, 240, 320) == 1
+    assert L.call("sd_conv3x3_bwd_fused_ok", 32, 32, 12, 96) == 0  # H % 8
+    assert L.call("sd_conv3x3_bwd_fused_ok", 64, 32, 240, 320) == 0
+    assert L.call("sd_conv3x3_bwd_fused_splits", 64, 240, 320) == 256
+    assert L.call("sd_conv3x3_bwd_fused_splits", 1, 16, 32) == 8  # 2 tiles: a multiple of 8 blocks (the XCD map)
 
 
 def test_fused_bn_wgrad_host_validation():
