@@ -11,11 +11,12 @@
 //
 // One 512-thread block per CU, persistent over a contiguous range of 8x16-pixel tiles (its split-K range):
 //   waves 4-7 (loaders): per tile, the 10x18 halo of (da, y) -> dy and of y_prev -> x (BN + ReLU), through registers
-//                        (two tiles in flight) into an LDS double buffer;
-//   waves 0-3 (MFMA)   : weight gradient (16 co x 16 ci per wave, v_mfma_f32_16x16x32_bf16 on transposed fragments,
-//                        k = tile pixels) and dgrad (32 tile pixels = two rows per wave, all 32 ci, 32x32x16 MFMAs over
-//                        9 taps x 32 dy channels with the dgrad weights resident in LDS), then the dgrad epilogue
-//                        (the sums read the raw y_prev from L2).
+//                        (two tiles in flight) into an LDS double buffer, plus the raw y_prev of the tile (the
+//                        sums' operand);
+//   waves 0-3 (MFMA)   : weight gradient (two taps and a quarter of the third per wave, 32 co x 32 ci,
+//                        v_mfma_f32_32x32x16_bf16 on transposed fragments, k = tile pixels) and dgrad (32 tile
+//                        pixels = two rows per wave, all 32 ci, 32x32x16 MFMAs over 9 taps x 32 dy channels with the
+//                        dgrad weights resident in LDS), then the dgrad epilogue.
 #include <stdio.h>
 
 #include "halo_util.h"
@@ -33,12 +34,14 @@ static_assert(FB_TH * FB_TW == 128 && FB_TW % 16 == 0, "4 MFMA waves x 32 pixels
 constexpr int FB_DL = 40;                          // dy halo pixel pitch (80 B: odd 16-B slot count, b128 reads)
 constexpr int FB_XL = 48;                          // x halo pixel pitch (96 B: conflict-free transposed reads)
 constexpr int FB_WL = 9 * 32 + 8;                  // dgrad weight row (592 B, odd slot count)
-constexpr int FB_DYH = FB_HSL * FB_DL, FB_XH = FB_HSL * FB_XL;
-constexpr int FB_BUF = FB_DYH + FB_XH;             // elements per LDS buffer
+constexpr int FB_SL = 40;                          // raw y_prev stash pitch (the sums' operand)
+constexpr int FB_DYH = FB_HSL * FB_DL, FB_XH = FB_HSL * FB_XL, FB_ST = FB_TH * FB_TW * FB_SL;
+constexpr int FB_BUF = FB_DYH + FB_XH + FB_ST;     // elements per LDS buffer
 constexpr int FB_BLOCKS = 256;                     // one per CU
 #ifndef FB_EXP
 #define FB_EXP 0  // timing-only builds (results wrong): 1 no loader transform, 2 no wgrad, 4 no dgrad, 8 no dgrad
-                  // epilogue, 16 no loads after the first two tiles, 32 per-wave phase cycle counters (sd_debug_buffer)
+                  // epilogue, 16 no loads after the first two tiles, 32 per-wave phase cycle counters (sd_debug_buffer),
+                  // 128 loader waves at s_setprio 1
 #endif
 constexpr bool FB_DG = (FB_EXP & 32) != 0;
 __device__ __forceinline__ unsigned long long fb_clk() {
@@ -101,6 +104,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
     if (is_loader) {
         // =========================================================== loader waves
         const int ltid = tid - 256;
+        if (FB_EXP & 128) __builtin_amdgcn_s_setprio(1);  // experiment: the loaders win VALU issue arbitration
         const int piece = fb_piece<4>(ltid);  // fixed per thread (256 * i keeps (item >> 3) % 4)
         constexpr unsigned OOB = 0x80000000u;
         // this thread's 8 channels: this layer's folded BatchNorm-backward constants and the previous layer's affine
@@ -118,13 +122,16 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
         const float4 s1 = *reinterpret_cast<const float4*>(p.psc + piece * 8 + 4);
         const float4 t0 = *reinterpret_cast<const float4*>(p.psh + piece * 8);
         const float4 t1 = *reinterpret_cast<const float4*>(p.psh + piece * 8 + 4);
-        // halo geometry of the items: (row << 8 | col), ~0 past the halo
+        // halo geometry of the items: (row << 8 | col), ~0 past the halo; interior stash slot or -1
         unsigned geo[FB_NI];
+        int stash[FB_NI];
 #pragma unroll
         for (int i = 0; i < FB_NI; ++i) {
             const int px = fb_pixel<4>(ltid + 256 * i);
             const int hy = px / FB_HW, hx = px - hy * FB_HW;
             geo[i] = px < FB_HPX ? (unsigned)(hy << 8 | hx) : 0xffffffffu;
+            const bool in = px < FB_HPX && hy >= 1 && hy <= FB_TH && hx >= 1 && hx <= FB_TW;
+            stash[i] = in ? ((hy - 1) * FB_TW + hx - 1) * FB_SL + piece * 8 : -1;
         }
         // items FB_HPX * 4.. are past the halo: a loader wave whose first item of the last slot is past it skips that
         // slot (wave-uniform)
@@ -173,6 +180,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
         auto store = [&](Set& q, int buf) __attribute__((always_inline)) {
             __bf16* dyh = smem + buf * FB_BUF;
             __bf16* xh = dyh + FB_DYH;
+            __bf16* st = xh + FB_XH;
             auto put = [&](auto SEL) __attribute__((always_inline)) {
 #pragma unroll
                 for (int i = 0; i < FB_NI; ++i) {
@@ -187,6 +195,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
                     }
                     *reinterpret_cast<uint4*>(dyh + px * FB_DL + piece * 8) = d;
                     *reinterpret_cast<uint4*>(xh + px * FB_XL + piece * 8) = x;
+                    if (stash[i] >= 0) *reinterpret_cast<uint4*>(st + stash[i]) = q.x[i];  // raw y_prev (0 outside)
                 }
             };
             if (q.edge)
@@ -246,14 +255,20 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
 
     // =============================================================== MFMA waves
     __syncthreads();  // the resident weights
-    // weight gradient: wave (wc, wo) owns ci 16 wc .. +15 and co 16 wo .. +15 (the k_halo_wgrad_ws<32, 32> grid);
-    // transposed fragments: within a 16-lane group, lane 4q + pp supplies row q of pixel rows pc, pc + 8
+    // weight gradient, 32 co x 32 ci per tap (v_mfma_f32_32x32x16_bf16, k = 16 pixels = one tile row): wave w owns
+    // taps w and w + 4 over the tile's 8 rows and tap 8 over rows 2w, 2w + 1 (summed over the waves at the end).
+    // Transposed fragments (tr_pair): 16-lane group g holds channels 16 (g & 1) + (lane & 15) of the pixels
+    // 4 (g >> 1) + {0..3, 8..11} of the row (the MFMA's k-half g >> 1); lane 4q + pp supplies the address of pixel
+    // 4 (g >> 1) + q, channels 16 (g & 1) + 4 pp
     const int g = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
-    const int pc = 16 * (g >> 1) + 4 * (g & 1) + q4;
-    const int ci0 = 16 * (wid & 1), co0 = 16 * (wid >> 1);
-    f32x4 accw[9];
+    const int pk = 4 * (g >> 1) + q4, ch16 = 16 * (g & 1) + 4 * pp;
+    const int tw0 = wid, tw1 = wid + 4;
+    const int toffx0 = ((tw0 / 3) * FB_HW + tw0 % 3) * FB_XL, toffx1 = ((tw1 / 3) * FB_HW + tw1 % 3) * FB_XL;
+    f32x16 accw[3];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) accw[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accw[t][r] = 0.f;
     // dgrad epilogue: this lane's 8 channels (lane % 4) of the previous BatchNorm layer, for its sums
     BnsK bk[4];
     {
@@ -280,7 +295,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
     for (int j = 0; j < 16; ++j) own[j] = 0.f;
     __bf16* const scw = scr + wid * 32 * 32;
     auto swz = [](int j, int px) { return j ^ ((px >> 1) & 3); };
-    unsigned long long tc[4] = {0, 0, 0, 0}, t0 = 0, t_all = FB_DG ? fb_clk() : 0;
+    unsigned long long tc[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t_all = FB_DG ? fb_clk() : 0;
     auto stamp = [&](int k) __attribute__((always_inline)) {
         if (FB_DG) {
             const unsigned long long t1 = fb_clk();
@@ -288,50 +303,76 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             t0 = t1;
         }
     };
+    // dgrad epilogue of a tile (acc: its C^T[ci][px], yv: the raw y_prev pieces of its stores): lanes l / l + 32 hold
+    // the 4-channel halves of each 8-channel group of pixel l & 31; v_permlane32_swap pairs them into whole 16-B
+    // pieces, which go through the wave's scratch and leave as pixel rows (16 pixels x 4 pieces per store
+    // instruction), with the previous layer's BatchNorm-backward sums
+    auto epilogue = [&](const f32x16& acc, const uint4* yv, int tl) __attribute__((always_inline)) {
+        uint2 pk2[4];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            bf16x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[4 * g4 + q];
+            pk2[g4] = *reinterpret_cast<uint2*>(&v);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k += 2) {
+            const auto rx = __builtin_amdgcn_permlane32_swap(pk2[k].x, pk2[k + 1].x, false, false);
+            const auto ry = __builtin_amdgcn_permlane32_swap(pk2[k].y, pk2[k + 1].y, false, false);
+            const int px = lane & 31, j = k + (lane >> 5);
+            *reinterpret_cast<uint4*>(scw + px * 32 + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        }
+        asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
+        int tx, ty, b;
+        fb_tile(p, tl, tx, ty, b);
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.dx + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
+        uint4 vv[2];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int px = rr * 16 + (lane >> 2), j = lane & 3;
+            vv[rr] = *reinterpret_cast<const uint4*>(scw + px * 32 + swz(j, px) * 8);
+        }
+        asm volatile("" ::: "memory");  // the next tile's scratch writes after these reads
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int q = wid * 32 + rr * 16 + (lane >> 2), j = lane & 3;
+            const int h = ty * FB_TH + q / FB_TW, w = tx * FB_TW + q % FB_TW;  // inside the image (H % 8, W % 16)
+            bns_add(own, vv[rr], yv[rr], true, bk);
+            __attribute__((ext_vector_type(4))) unsigned data = {vv[rr].x, vv[rr].y, vv[rr].z, vv[rr].w};
+            __builtin_amdgcn_raw_buffer_store_b128(data, rd, (unsigned)(h * p.W + w) * 64u + (unsigned)j * 16u, 0, 2);
+        }
+    };
+    // software pipeline: tile it's weight-gradient MFMAs are issued before tile it - 1's epilogue (VALU, LDS, stores),
+    // which runs beside them; its raw y_prev pieces were read before the barrier that hands its buffer back
+    f32x16 accp;
+    uint4 yvp[2];
     for (int it = 0; it < ntile; ++it) {
         if (FB_DG) t0 = fb_clk();
         __syncthreads();  // tile it is in buffer it & 1
         stamp(0);
         const __bf16* dyh = smem + (it & 1) * FB_BUF;
         const __bf16* xh = dyh + FB_DYH;
-        // the raw y_prev of this wave's epilogue pieces (the sums' xhat and ReLU mask), from L2 (the loaders fetched
-        // them two tiles ago), in flight through the MFMA phases
-        const int tl = t_begin + it;
-        int tx, ty, b;
-        fb_tile(p, tl, tx, ty, b);
-        const int h0 = ty * FB_TH, w0 = tx * FB_TW;
-        uint4 yv[2];
-        {
-            const __amdgpu_buffer_rsrc_t ryp = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(p.yp + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
+        const __bf16* st = xh + FB_XH;  // the raw y_prev of the tile (the sums' xhat and ReLU mask)
+        // ---- weight gradient: k = the tile's pixels, one 16-pixel row per k-step
 #pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                const int q = wid * 32 + rr * 16 + (lane >> 2), j = lane & 3;  // tile pixel q
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-                    ryp, (unsigned)((h0 + q / FB_TW) * p.W + w0 + q % FB_TW) * 64u + (unsigned)j * 16u, 0, 0);
-                yv[rr] = make_uint4(v[0], v[1], v[2], v[3]);
-            }
-        }
-        // ---- weight gradient: k = the tile's pixels, 4 k-steps of 32 (tile pixels q = 32 ks + pc, + 8: one row)
-#pragma unroll
-        for (int ks = 0; ks < ((FB_EXP & 2) ? 0 : 4); ++ks) {
-            const int q = ks * 32 + pc, r = q / FB_TW, c = q % FB_TW;
-            const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + c) * FB_DL + co0 + 4 * pp;  // dy^T
+        for (int r = 0; r < ((FB_EXP & 2) ? 0 : FB_TH); ++r) {
+            const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + pk) * FB_DL + ch16;  // dy^T of row r
             const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
-            bf16x8 bf[9];
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const __bf16* x0 = xh + ((r + tap / 3) * FB_HW + tap % 3 + c) * FB_XL + ci0 + 4 * pp;
-                bf[tap] = tr_pair(x0, x0 + 8 * FB_XL);
+            const __bf16* xr = xh + (r * FB_HW + pk) * FB_XL + ch16;
+            const bf16x8 b0 = tr_pair(xr + toffx0, xr + toffx0 + 8 * FB_XL);
+            const bf16x8 b1 = tr_pair(xr + toffx1, xr + toffx1 + 8 * FB_XL);
+            accw[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, accw[0], 0, 0, 0);
+            accw[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, accw[1], 0, 0, 0);
+            if ((r >> 1) == wid) {  // tap 8 on this wave's two rows
+                const __bf16* x8 = xr + (2 * FB_HW + 2) * FB_XL;
+                accw[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_pair(x8, x8 + 8 * FB_XL), accw[2], 0, 0, 0);
             }
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap)
-                accw[tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[tap], accw[tap], 0, 0, 0);
         }
-        if (FB_DG) {  // the weight gradient's MFMAs retired
-            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-            stamp(1);
-        }
+        stamp(1);
+        if (it > 0 && !(FB_EXP & 8)) epilogue(accp, yvp, t_begin + it - 1);
+        stamp(3);
         // ---- dgrad of tile pixels 32 wid ..: C^T[ci][px] over 9 taps x 2 k-steps of 16 dy channels
         f32x16 accd;
 #pragma unroll
@@ -350,72 +391,37 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
                 accd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, accd, 0, 0, 0);
             }
         }
-        if (FB_DG) {
-            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-            stamp(2);
+        accp = accd;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int px = rr * 16 + (lane >> 2), j = lane & 3;
+            yvp[rr] = *reinterpret_cast<const uint4*>(st + (wid * 32 + px) * FB_SL + j * 8);
         }
-        // ---- dgrad epilogue: lanes l / l + 32 hold the 4-channel halves of each 8-channel group of pixel l & 31;
-        // v_permlane32_swap pairs them into whole 16-B pieces, which go through the wave's scratch and leave as
-        // pixel rows (16 pixels x 4 pieces per store instruction), with the previous layer's BatchNorm-backward sums
-        if (!(FB_EXP & 8)) {
-            uint2 pk[4];
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                bf16x4 v;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = (__bf16)accd[4 * g4 + q];
-                pk[g4] = *reinterpret_cast<uint2*>(&v);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k += 2) {
-                const auto rx = __builtin_amdgcn_permlane32_swap(pk[k].x, pk[k + 1].x, false, false);
-                const auto ry = __builtin_amdgcn_permlane32_swap(pk[k].y, pk[k + 1].y, false, false);
-                const int px = lane & 31, j = k + (lane >> 5);
-                *reinterpret_cast<uint4*>(scw + px * 32 + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-            }
-            asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
-            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(p.dx + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
-            uint4 vv[2];
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                const int px = rr * 16 + (lane >> 2), j = lane & 3;
-                vv[rr] = *reinterpret_cast<const uint4*>(scw + px * 32 + swz(j, px) * 8);
-            }
-            asm volatile("" ::: "memory");  // the next tile's scratch writes after these reads
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                const int q = wid * 32 + rr * 16 + (lane >> 2), j = lane & 3;
-                const int h = h0 + q / FB_TW, w = w0 + q % FB_TW;
-                const bool live = (h < p.H) & (w < p.W);
-                bns_add(own, vv[rr], yv[rr], live, bk);
-                __attribute__((ext_vector_type(4))) unsigned data = {vv[rr].x, vv[rr].y, vv[rr].z, vv[rr].w};
-                const unsigned off = live ? (unsigned)(h * p.W + w) * 64u + (unsigned)j * 16u : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b128(data, rd, off, 0, 2);
-            }
-        } else if (accd[0] == 1.2345e-30f) {  // timing build: keep the dgrad MFMAs live
-            p.dx[lane] = (__bf16)accd[1];
-        }
-        stamp(3);
+        stamp(2);
     }
+    if (ntile > 0 && !(FB_EXP & 8)) epilogue(accp, yvp, t_begin + ntile - 1);
     if (FB_DG && p.dbg && lane == 0) {
         unsigned long long* d = p.dbg + ((size_t)bid * 8 + wid) * 8;
-        d[0] = tc[0];
-        d[1] = tc[1];
-        d[2] = tc[2];
-        d[3] = tc[3];
-        d[4] = fb_clk() - t_all;
-        d[5] = ntile;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = tc[k];
+        d[6] = fb_clk() - t_all;
+        d[7] = ntile;
     }
     if (ntile & 1) __syncthreads();  // the loaders' last (even-count) iteration
 
-    // weight-gradient partial slab: slab[bid][co][tap * 32 + ci]   (16x16 C layout: row 4 (lane >> 4) + r, col lane & 15)
+    // weight-gradient partial slab: slab[bid][co][tap * 32 + ci]   (32x32 C layout: element i of lane l is row
+    // co = 8 (i / 4) + 4 (l / 32) + i % 4, column ci = l % 32); tap 8's four wave partials go through the LDS buffer
+    // the last tile is not in (the loaders are past their last store; other MFMA waves may still read the last tile)
     float* slab = p.slab + (size_t)bid * 32 * 288;
+    float* red8 = reinterpret_cast<float*>(smem + (ntile & 1) * FB_BUF);
+    static_assert(FB_BUF * 2 >= 4 * 1024 * 4, "tap-8 partials fit one halo buffer");
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            slab[(size_t)(co0 + 4 * (lane >> 4) + r) * 288 + tap * 32 + ci0 + (lane & 15)] = accw[tap][r];
+    for (int i = 0; i < 16; ++i) {
+        const int co = 8 * (i / 4) + 4 * (lane >> 5) + i % 4, ci = lane & 31;
+        slab[(size_t)co * 288 + tw0 * 32 + ci] = accw[0][i];
+        slab[(size_t)co * 288 + tw1 * 32 + ci] = accw[1][i];
+        red8[wid * 1024 + co * 32 + ci] = accw[2][i];
+    }
     // the previous layer's BatchNorm-backward sums: lanes l, l + 4, ... hold the same 8 channels
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -427,6 +433,9 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             redf[(wid * 32 + lane * 8 + k / 2) * 2 + (k & 1)] = own[(k & ~3) | ((k & 1) << 1) | ((k >> 1) & 1)];
     }
     __syncthreads();
+#pragma unroll
+    for (int e = tid; e < 1024; e += 256)
+        slab[(size_t)(e >> 5) * 288 + 8 * 32 + (e & 31)] = (red8[e] + red8[1024 + e]) + (red8[2048 + e] + red8[3072 + e]);
     if (tid < 32) {
         float s = 0.f, sx = 0.f;
 #pragma unroll

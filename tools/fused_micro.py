@@ -59,10 +59,10 @@ def main():
         L.call("sd_conv3x3_bwd_fused", *args)
         torch.cuda.synchronize()
         d = dbg.view(sp, 8, 8).double().cpu()
-        nt = d[:, 0, 5].sum()
-        mf = d[:, :4, :5].sum(dim=(0, 1)) / (4 * nt)
+        nt = d[:, 0, 7].sum()
+        mf = d[:, :4, :7].sum(dim=(0, 1)) / (4 * nt)
         ld = d[:, 4:, :5].sum(dim=(0, 1)) / (4 * nt)
-        out["mfma_per_tile"] = dict(zip(["barrier", "wgrad", "dgrad", "epilogue", "total"], mf.round().tolist()))
+        out["mfma_per_tile"] = dict(zip(["barrier", "wgrad", "dgrad", "epi_bns_store", "epi_cvt_scratch", "epi_read", "total"], mf.round().tolist()))
         out["loader_per_tile"] = dict(zip(["transform_store", "load_issue", "barrier", "load_wait", "total"], ld.round().tolist()))
     print(json.dumps(out))
 
