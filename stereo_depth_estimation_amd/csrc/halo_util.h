@@ -8,8 +8,9 @@ namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// halo_finish_pk's transform on an explicit per-channel affine (8 channels: s0|s1 scales, h0|h1 shifts), in packed
-// fp32 pairs (v_pk_fma_f32: the same fma per channel)
+// halo_finish_pk's transform on an explicit per-channel affine (8 channels: s0|s1 scales, h0|h1 shifts). One
+// v_fma_f32 per channel: packed v_pk_fma_f32 pairs measured 2.2 % slower over the bench step (these loaders run
+// beside MFMA waves on the same SIMDs, where packed fp32 VALU issues slower than two scalar ops)
 __device__ __forceinline__ uint4 bnrelu_pk(uint4 raw, float4 s0, float4 s1, float4 h0, float4 h1) {
     const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
     const f32x2 s[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
@@ -18,8 +19,8 @@ __device__ __forceinline__ uint4 bnrelu_pk(uint4 raw, float4 s0, float4 s1, floa
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const f32x2 v = {__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
-        const f32x2 r = __builtin_elementwise_fma(v, s[i], h[i]);
-        asm("v_cvt_pk_bf16_f32 %0, %1, %2\n\tv_pk_max_i16 %0, %0, 0" : "=v"(o[i]) : "v"(r.x), "v"(r.y));
+        const float rx = __builtin_fmaf(v.x, s[i].x, h[i].x), ry = __builtin_fmaf(v.y, s[i].y, h[i].y);
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2\n\tv_pk_max_i16 %0, %0, 0" : "=v"(o[i]) : "v"(rx), "v"(ry));
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
@@ -67,7 +68,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* a0, const __bf16* a1) {
 // dy = k0*(dz - k1 - xhat*k2), dz = da where z = y*scale+shift > 0 (the forward ReLU mask, recomputed as
 // k_bn_bwd_apply does), xhat = (y-mean)*invstd, written in terms of z (which the mask needs anyway) with
 // k0 = scale: dy = scale*dz + Bz*z + Cz, Bz = -invstd*k2, Cz = invstd*k2*shift + scale*(mean*invstd*k2 - k1);
-// channel pairs in packed fp32 (v_pk_fma_f32), the mask applied to da
+// the mask applied to da (scalar fp32, as bnrelu_pk)
 __device__ __forceinline__ uint4 bn_bwd_pk(uint4 da, uint4 y, const float* sc, const float* sh, const float* Bz,
                                            const float* Cz) {
     const unsigned dw[4] = {da.x, da.y, da.z, da.w}, yw[4] = {y.x, y.y, y.z, y.w};
@@ -77,12 +78,14 @@ __device__ __forceinline__ uint4 bn_bwd_pk(uint4 da, uint4 y, const float* sc, c
         const f32x2 s2 = {sc[2 * i], sc[2 * i + 1]}, h2 = {sh[2 * i], sh[2 * i + 1]};
         const f32x2 b2 = {Bz[2 * i], Bz[2 * i + 1]}, c2 = {Cz[2 * i], Cz[2 * i + 1]};
         const f32x2 yv = {__uint_as_float(yw[i] << 16), __uint_as_float(yw[i] & 0xffff0000u)};
-        f32x2 dv = {__uint_as_float(dw[i] << 16), __uint_as_float(dw[i] & 0xffff0000u)};
-        const f32x2 z = __builtin_elementwise_fma(yv, s2, h2);
-        const f32x2 t = __builtin_elementwise_fma(b2, z, c2);
-        dv.x = z.x > 0.f ? dv.x : 0.f;
-        dv.y = z.y > 0.f ? dv.y : 0.f;
-        const f32x2 r = __builtin_elementwise_fma(s2, dv, t);
+        const f32x2 dv = {__uint_as_float(dw[i] << 16), __uint_as_float(dw[i] & 0xffff0000u)};
+        f32x2 r;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float z = __builtin_fmaf(yv[h], s2[h], h2[h]);
+            const float t = __builtin_fmaf(b2[h], z, c2[h]);
+            r[h] = __builtin_fmaf(s2[h], z > 0.f ? dv[h] : 0.f, t);
+        }
         asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(o[i]) : "v"(r.x), "v"(r.y));
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
