@@ -91,6 +91,9 @@ class GemmTimer:
         if name == "sd_conv3x3_bwd_fused":  # weight gradient + dgrad of a 32 -> 32 full-resolution conv, one pass
             B, H, W = args[14:17]
             return 2.0 * 2.0 * B * H * W * 32 * 9 * 32, "k_bwd_fused32"
+        if name == "sd_conv3x3_bwd_fused_dec":  # the same for dec1.0 (64 -> 32 channels)
+            B, H, W = args[13:16]
+            return 2.0 * 2.0 * B * H * W * 32 * 9 * 64, "k_bwd_fused_dec"
         xin = eng.ws.t["xin"].data_ptr()
         if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             dt, src, B, H, W, _, N = args[:7]
@@ -113,7 +116,7 @@ class GemmTimer:
 
     def __call__(self, name, args, phase):
         if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd",
-                        "sd_conv3x3_bwd_fused"):
+                        "sd_conv3x3_bwd_fused", "sd_conv3x3_bwd_fused_dec"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
         ev.record(self._stream(args[-1]))  # the launch stream (SD_SIDE_REDUCE=2 puts some GEMMs on a second one)
@@ -127,6 +130,8 @@ class GemmTimer:
             nbytes = self._min_bytes(args) if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum") else 0.0
             if name == "sd_conv3x3_bwd_fused":  # da, y, y_prev read, dx written once (bf16, 32 channels)
                 nbytes = 4.0 * args[14] * args[15] * args[16] * 32 * 2
+            if name == "sd_conv3x3_bwd_fused_dec":  # da, y, u, y_skip read, d(u), d(skip) written once
+                nbytes = 6.0 * args[13] * args[14] * args[15] * 32 * 2
             self.pending.append((kname, flops, start, ev, name, self._shape(name, args), nbytes))
             if name == "sd_conv_gemm" and self._last_phase == "fwd":
                 # forward order (model.py:79-104): the first 10 3x3 convs are enc1..enc4, bottleneck
@@ -182,6 +187,8 @@ class GemmTimer:
     def _shape(name, args):
         if name == "sd_conv3x3_bwd_fused":
             return f"bwd_fused P={args[14] * args[15] * args[16]} C=32"
+        if name == "sd_conv3x3_bwd_fused_dec":
+            return f"bwd_fused_dec P={args[13] * args[14] * args[15]} C=64->32"
         if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             s = args[1]
             return f"fwd M={args[2] * args[3] * args[4]} N={args[6]} K={s.taps}x{s.chans[0] + s.chans[1]}"

@@ -343,6 +343,17 @@ int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* scale, cons
                          const float* invstd, const float* coef, const void* yp, const float* pscale,
                          const float* pshift, const float* pmean, const float* pinvstd, const void* wd, int kpad,
                          int batch, int H, int W, void* dx, float* slab, float* partials, sd_stream s);
+/* The same for the full-resolution decoder conv0 (model.py:89-95, dec1.0: cat(u, relu(sscale*xs + sshift)), 32 + 32
+ * -> 32 channels): dy from (da, y) as above; the weight gradient as slab[splits][32][576] (k = tap*64 + ci, ci < 32 the
+ * u half; sd_wgrad_reduce with SD_W_CONV3, ci_real 64); the 64-channel dgrad (wd: [64][kpad], kpad >= 288) stored
+ * split, du = its first 32 channels (d(u), the ConvTranspose2d output gradient), dskip the other 32; and the column
+ * sums of du (the ConvTranspose2d bias gradient) as partials[splits][32] float2 (sum, 0) for sd_stat_rows_sum(ld 32).
+ * Replaces sd_wgrad_gemm_bnbwd (two 32-channel x blocks) + the SD_EPI_SPLIT_STATS dgrad. */
+int sd_conv3x3_bwd_fused_dec_ok(int C, int Cu, int Cs, int H, int W);
+int sd_conv3x3_bwd_fused_dec(const void* da, const void* y, const float* scale, const float* shift, const float* mean,
+                             const float* invstd, const float* coef, const void* xu, const void* xs,
+                             const float* sscale, const float* sshift, const void* wd, int kpad, int batch, int H,
+                             int W, void* du, void* dskip, float* slab, float* partials, sd_stream s);
 
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----
  * One flat fp32 parameter/gradient/state buffer (all tensors share lr/betas/eps/wd).

@@ -228,8 +228,9 @@ class UNetEngine:
         # (sd_conv_gemm_bnsum; SD_BNSUM_FUSE=0: sd_bn_bwd_reduce pass)
         self.bnsum_fuse = os.environ.get("SD_BNSUM_FUSE", "1") != "0"
         # bf16 training: the whole backward of the full-resolution 32 -> 32 conv1 layers (enc1.1, dec1.1) in one pass
-        # (sd_conv3x3_bwd_fused: dy stays in LDS; SD_BWD_FUSE=0: weight gradient + dgrad launches)
-        self.bwd_fuse = os.environ.get("SD_BWD_FUSE", "1") != "0"
+        # (sd_conv3x3_bwd_fused / _dec: dy stays in LDS; SD_BWD_FUSE=0: weight gradient + dgrad launches;
+        # SD_BWD_FUSE=1: the conv1 layers only)
+        self.bwd_fuse = {"0": 0, "1": 1}.get(os.environ.get("SD_BWD_FUSE", "2"), 2)
         self._bnsum_rows: dict[str, int] = {}
         # training: the split-K slab reduce of every weight gradient on a second stream (SD_SIDE_REDUCE=1), so it
         # overlaps the next layer's kernels instead of adding a kernel boundary to the critical path; 2: the
@@ -382,6 +383,8 @@ class UNetEngine:
             if train and cl.blk in UP_OF_DEC and cl.idx == 0:  # dgrad SPLIT_STATS rows (ConvTranspose bias grad)
                 rows = L.call("sd_conv_gemm_stat_rows", dt, B, H >> cl.level, W >> cl.level, cl.cin)
                 max_stat = max(max_stat, rows * cl.cin * 2)
+                # or the fused dec1.0 backward's d(up) column-sum rows (sd_conv3x3_bwd_fused_dec)
+                max_stat = max(max_stat, L.call("sd_conv3x3_bwd_fused_splits", B, H, W) * 32 * 2)
         t["stats"] = torch.empty(max_stat, dtype=f32, device=dev)
         for u in self.ups.values():
             t["u:" + u.name] = act(u.level - 1, u.cout)
@@ -468,12 +471,21 @@ class UNetEngine:
         self.ws = ws
         return ws
 
-    def _bwd_fused(self, cl: ConvL, H: int, W: int) -> bool:
-        """Whether conv `cl`'s backward runs as one sd_conv3x3_bwd_fused pass (bf16 training, a 32 -> 32 conv1 whose
-        input is its block's conv0 output, at a tiling the kernel takes: enc1.1 and dec1.1 at full resolution)."""
-        return (self.bwd_fuse and self.sd_dtype == L.SD_BF16 and cl.idx == 1 and cl.cout == 32 and cl.cin == 32
-                and self.bnsum_fuse and L.call("sd_conv3x3_bwd_fused_ok", cl.cout, cl.cin, H >> cl.level,
-                                               W >> cl.level) == 1)
+    def _bwd_fused(self, cl: ConvL, H: int, W: int) -> int:
+        """Whether conv `cl`'s backward runs as one fused pass (bf16 training, at a tiling the kernels take):
+        1: sd_conv3x3_bwd_fused, a 32 -> 32 conv1 whose input is its block's conv0 output (enc1.1, dec1.1);
+        2: sd_conv3x3_bwd_fused_dec, a decoder conv0 on cat(32-channel up, 32-channel skip) -> 32 (dec1.0)."""
+        if not self.bwd_fuse or self.sd_dtype != L.SD_BF16:
+            return 0
+        Hl, Wl = H >> cl.level, W >> cl.level
+        if cl.idx == 1 and cl.cout == 32 and cl.cin == 32 and self.bnsum_fuse:
+            return 1 if L.call("sd_conv3x3_bwd_fused_ok", cl.cout, cl.cin, Hl, Wl) == 1 else 0
+        if cl.idx == 0 and cl.blk in UP_OF_DEC and self.bwd_fuse >= 2:
+            up, sk = self.ups[UP_OF_DEC[cl.blk]], self.convs[SKIP_OF_DEC[cl.blk] + ".1"]
+            if cl.cin == up.cout + sk.cout and L.call("sd_conv3x3_bwd_fused_dec_ok", cl.cout, up.cout, sk.cout, Hl,
+                                                      Wl) == 1:
+                return 2
+        return 0
 
     def _conv_splits(self, cl: ConvL, B: int, H: int, W: int) -> int:
         """Split-K slabs of conv `cl`'s weight gradient (its slab region holds the larger of the two kernels')."""
@@ -1046,7 +1058,27 @@ class UNetEngine:
     def _conv_bwd(self, cl: ConvL, need_dgrad: bool, fused_rows: int = 0):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         Hl, Wl = ws.H >> cl.level, ws.W >> cl.level
-        if need_dgrad and self._bwd_fused(cl, ws.H, ws.W):
+        kind = self._bwd_fused(cl, ws.H, ws.W) if need_dgrad else 0
+        if kind == 2:
+            # one pass: dy = BatchNorm-backward(da, y) staged in LDS, the weight gradient's split-K slabs over
+            # x = cat(u, relu(bn(y_skip))), the dgrad split into d(u) and d(skip), and d(u)'s column sums (the
+            # ConvTranspose2d bias gradient, for _up_bwd): da, y, u, y_skip read once, no dy round trip
+            self._bn_bwd(cl, fused_rows, apply=False)
+            up, sk = self.ups[UP_OF_DEC[cl.blk]], self.convs[SKIP_OF_DEC[cl.blk] + ".1"]
+            ssc, ssh = self._bn(sk)
+            sp = L.call("sd_conv3x3_bwd_fused_splits", ws.B, Hl, Wl)
+            args = (t["da:" + cl.name].data_ptr(), t["y:" + cl.name].data_ptr(), t["scale:" + cl.name].data_ptr(),
+                    t["shift:" + cl.name].data_ptr(), t["mean:" + cl.name].data_ptr(),
+                    t["invstd:" + cl.name].data_ptr(), t["coef:" + cl.name].data_ptr(), t["u:" + up.name].data_ptr(),
+                    t["y:" + sk.name].data_ptr(), ssc.data_ptr(), ssh.data_ptr(), self._wp(cl.off_d), cl.kpad_d,
+                    ws.B, Hl, Wl, t["du:" + up.name].data_ptr(), t["dskip:" + up.name].data_ptr())
+            self._wgrad_slabs(lambda slab, st: L.call("sd_conv3x3_bwd_fused_dec", *args, slab,
+                                                      t["stats"].data_ptr(), st),
+                              sp, cl.cout, 9 * cl.cin_pad, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key],
+                              gemm_may_side=False, key=cl.name)
+            self._up_bias_rows = (sp, 32)
+            return
+        if kind == 1:
             # one pass: dy = BatchNorm-backward(da, y) staged in LDS, the weight gradient's split-K slabs, the dgrad
             # into da of conv0 and conv0's BatchNorm-backward sums (4 full-resolution tensor passes instead of 7)
             self._bn_bwd(cl, fused_rows, apply=False)

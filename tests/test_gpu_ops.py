@@ -966,3 +966,55 @@ def test_conv3x3_bwd_fused_matches_reference(B, H, W):
     s_ref = torch.stack([dzp.sum((0, 2, 3)), (dzp * xh).sum((0, 2, 3))], 1)
     s_got = part.double().sum(0).cpu()
     assert float((s_got - s_ref).abs().max()) <= 1e-2 * (1 + float(s_ref.abs().max()))
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 16, 64), (1, 8, 16), (3, 24, 48)])
+def test_conv3x3_bwd_fused_dec_matches_reference(B, H, W):
+    """sd_conv3x3_bwd_fused_dec (dec1.0's backward in one pass) against fp64 PyTorch on the same bf16 operands:
+    dy = BatchNorm-backward(da, y) (staged as bf16), x = cat(u, relu(bn_skip(y_skip))) (bf16),
+    dW = conv2d_weight(x, dy), dx = conv2d_input(dy, W) stored bf16 as d(u) | d(skip), and the column sums of the
+    stored d(u) (the ConvTranspose2d bias gradient). Bounds as test_conv3x3_bwd_fused_matches_reference."""
+    lib = L()
+    torch.manual_seed(37)
+    C = 32
+    bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    da, y = bf(torch.randn(B, C, H, W)), bf(torch.randn(B, C, H, W))
+    u, ys = bf(torch.randn(B, C, H, W)), bf(torch.randn(B, C, H, W))
+    sc, sh = torch.rand(C).double() + 0.5, torch.randn(C).double() * 0.3
+    sc[::7] *= -1
+    mu, is_ = torch.randn(C).double() * 0.2, torch.rand(C).double() + 0.5
+    coef = torch.randn(C, 3).double() * 0.1
+    ssc, ssh = torch.rand(C).double() + 0.5, torch.randn(C).double() * 0.3
+    w = (torch.randn(C, 2 * C, 3, 3) / 24.0).to(torch.bfloat16).double()
+    v = lambda t: t[None, :, None, None]  # noqa: E731
+    z = y * v(sc) + v(sh)
+    dz = torch.where(z > 0, da, torch.zeros_like(da))
+    dy = bf((v(sc) * (dz - v(coef[:, 1]) - v(coef[:, 2]) * (y - v(mu)) * v(is_))).float())
+    x = torch.cat([u, bf(torch.relu(ys * v(ssc) + v(ssh)).float())], 1)
+    dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, padding=1)
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=1)
+    f32 = lambda t: t.float().contiguous().to(DEV)  # noqa: E731
+    wp, kpad = _pack3(w.float(), 2 * C, True, "bf16")
+    sp = lib.call("sd_conv3x3_bwd_fused_splits", B, H, W)
+    assert lib.call("sd_conv3x3_bwd_fused_dec_ok", C, C, C, H, W) == 1
+    slab = torch.full((sp * C * 9 * 2 * C,), float("nan"), device=DEV)
+    part = torch.full((sp, C, 2), float("nan"), device=DEV)
+    du = torch.full((B * H * W, C), float("nan"), dtype=torch.bfloat16, device=DEV)
+    dsk = torch.full((B * H * W, C), float("nan"), dtype=torch.bfloat16, device=DEV)
+    tens = [_nhwc(t.float(), "bf16") for t in (da, y, u, ys)]
+    prm = [f32(t) for t in (sc, sh, mu, is_, coef, ssc, ssh)]
+    lib.call("sd_conv3x3_bwd_fused_dec", tens[0].data_ptr(), tens[1].data_ptr(), *[t.data_ptr() for t in prm[:5]],
+             tens[2].data_ptr(), tens[3].data_ptr(), prm[5].data_ptr(), prm[6].data_ptr(), wp.data_ptr(), kpad, B, H,
+             W, du.data_ptr(), dsk.data_ptr(), slab.data_ptr(), part.data_ptr(), lib.stream_handle())
+    dw = torch.empty(C, 2 * C, 3, 3, device=DEV)
+    lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, C, 9 * 2 * C, lib.SD_W_CONV3, 2 * C, dw.data_ptr(),
+             lib.stream_handle())
+    bias = torch.empty(C, device=DEV)
+    lib.call("sd_stat_rows_sum", part.data_ptr(), sp, C, C, bias.data_ptr(), lib.stream_handle())
+    torch.cuda.synchronize()
+    dw = dw.double().cpu()
+    assert float((dw - dw_ref).abs().max()) <= 1e-3 * float(dw_ref.abs().max())
+    got = torch.cat([_from_nhwc(du, B, H, W, C), _from_nhwc(dsk, B, H, W, C)], 1).double()
+    assert float(((got - dx_ref).abs() - 2.0 ** -7 * dx_ref.abs()).max()) <= 1e-3 * float(dx_ref.abs().max())
+    b_ref = got[:, :C].sum((0, 2, 3))
+    assert float((bias.double().cpu() - b_ref).abs().max()) <= 1e-4 * (1 + float(b_ref.abs().max()))

@@ -106,6 +106,8 @@ def test_planning_queries_are_host_only():
     assert L.call("sd_conv3x3_bwd_fused_ok", 64, 32, 240, 320) == 0
     assert L.call("sd_conv3x3_bwd_fused_splits", 64, 240, 320) == 256
     assert L.call("sd_conv3x3_bwd_fused_splits", 1, 16, 32) == 8  # 2 tiles: a multiple of 8 blocks (the XCD map)
+    assert L.call("sd_conv3x3_bwd_fused_dec_ok", 32, 32, 32, 240, 320) == 1  # dec1.0: cat(32 up, 32 skip) -> 32
+    assert L.call("sd_conv3x3_bwd_fused_dec_ok", 32, 64, 32, 240, 320) == 0
 
 
 def test_fused_bn_wgrad_host_validation():
