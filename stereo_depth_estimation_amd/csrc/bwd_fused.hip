@@ -42,9 +42,8 @@ constexpr int FB_DYH = FB_HSL * FB_DL, FB_XH = FB_HSL * FB_XL, FB_ST = FB_TH * F
 constexpr int FB_BUF = FB_DYH + FB_XH + FB_ST;     // elements per LDS buffer
 constexpr int FB_BLOCKS = 256;                     // one per CU
 #ifndef FB_EXP
-#define FB_EXP 0  // timing-only builds (results wrong): 1 no loader transform, 2 no wgrad, 4 no dgrad, 8 no dgrad
-                  // epilogue, 16 no loads after the first two tiles, 32 per-wave phase cycle counters (sd_debug_buffer),
-                  // 128 loader waves at s_setprio 1
+#define FB_EXP 0  // timing-only builds (results wrong): 1 no loader transform, 16 no loads after the first two
+                  // tiles, 32 per-wave phase cycle counters (sd_debug_buffer), 128 loader waves at s_setprio 1
 #endif
 constexpr bool FB_DG = (FB_EXP & 32) != 0;
 __device__ __forceinline__ unsigned long long fb_clk() {
@@ -347,20 +346,22 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             __builtin_amdgcn_raw_buffer_store_b128(data, rd, (unsigned)(h * p.W + w) * 64u + (unsigned)j * 16u, 0, 2);
         }
     };
-    // software pipeline: tile it's weight-gradient MFMAs are issued before tile it - 1's epilogue (VALU, LDS, stores),
-    // which runs beside them; its raw y_prev pieces were read before the barrier that hands its buffer back
+    // software pipeline: tile it - 1's epilogue (VALU, LDS, stores) sits between tile it's weight-gradient MFMAs in one
+    // branch-free block (the first tile peeled), so its VALU issues in the MFMAs' shadow; its raw y_prev pieces were
+    // read before the barrier that hands its buffer back
     f32x16 accp;
     uint4 yvp[2];
-    for (int it = 0; it < ntile; ++it) {
+    auto tile = [&](int it, auto EPI) __attribute__((always_inline)) {
         if (FB_DG) t0 = fb_clk();
         __syncthreads();  // tile it is in buffer it & 1
         stamp(0);
         const __bf16* dyh = smem + (it & 1) * FB_BUF;
         const __bf16* xh = dyh + FB_DYH;
         const __bf16* st = xh + FB_XH;  // the raw y_prev of the tile (the sums' xhat and ReLU mask)
-        // ---- weight gradient: k = the tile's pixels, one 16-pixel row per k-step
+        // ---- weight gradient: k = the tile's pixels, one 16-pixel row per k-step; this wave's two tap-8 rows first
 #pragma unroll
-        for (int r = 0; r < ((FB_EXP & 2) ? 0 : FB_TH); ++r) {
+        for (int rr = 0; rr < FB_TH; ++rr) {
+            const int r = (2 * wid + rr) & (FB_TH - 1);
             const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + pk) * FB_DL + ch16;  // dy^T of row r
             const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
             const __bf16* xr = xh + (r * FB_HW + pk) * FB_XL + ch16;
@@ -368,14 +369,14 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             const bf16x8 b1 = tr_pair(xr + toffx1, xr + toffx1 + 8 * FB_XL);
             accw[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, accw[0], 0, 0, 0);
             accw[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, accw[1], 0, 0, 0);
-            if ((r >> 1) == wid) {  // tap 8 on this wave's two rows
+            if (rr < 2) {  // tap 8 on rows 2 wid, 2 wid + 1
                 const __bf16* x8 = xr + (2 * FB_HW + 2) * FB_XL;
                 accw[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_pair(x8, x8 + 8 * FB_XL), accw[2], 0, 0, 0);
             }
+            if constexpr (decltype(EPI)::v)
+                if (rr == 2) epilogue(accp, yvp, t_begin + it - 1);
         }
         stamp(1);
-        if (it > 0 && !(FB_EXP & 8)) epilogue(accp, yvp, t_begin + it - 1);
-        stamp(3);
         // ---- dgrad of tile pixels 32 wid ..: C^T[ci][px] over 9 taps x 2 k-steps of 16 dy channels
         f32x16 accd;
 #pragma unroll
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
         const int qd = wid * 32 + (lane & 31);
         const __bf16* drow = dyh + ((qd / FB_TW) * FB_HW + qd % FB_TW) * FB_DL + c8;
 #pragma unroll
-        for (int tap = 0; tap < ((FB_EXP & 4) ? 0 : 9); ++tap) {
+        for (int tap = 0; tap < 9; ++tap) {
             const int toff = ((tap / 3) * FB_HW + tap % 3) * FB_DL;
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
@@ -401,8 +402,10 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             yvp[rr] = *reinterpret_cast<const uint4*>(st + (wid * 32 + px) * FB_SL + j * 8);
         }
         stamp(2);
-    }
-    if (ntile > 0 && !(FB_EXP & 8)) epilogue(accp, yvp, t_begin + ntile - 1);
+    };
+    if (ntile > 0) tile(0, BoolC<false>{});
+    for (int it = 1; it < ntile; ++it) tile(it, BoolC<true>{});
+    if (ntile > 0) epilogue(accp, yvp, t_begin + ntile - 1);
     if (FB_DG && p.dbg && lane == 0) {
         unsigned long long* d = p.dbg + ((size_t)bid * 8 + wid) * 8;
 #pragma unroll
@@ -478,6 +481,7 @@ struct DecArgs {
     __bf16 *du, *dsk;                       // [B*H*W][32] each
     float* slab;                            // [blocks][32 co][576], k = tap*64 + ci
     float2* part;                           // [blocks][32]: (sum d(up), 0) per channel
+    unsigned long long* dbg;                // timing build only: [block][wave][8] phase cycles
 };
 constexpr int FD_BUF = FB_DYH + 2 * FB_XH;  // dy, x_up, x_skip halos
 
@@ -609,13 +613,37 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
         __builtin_amdgcn_sched_barrier(0);
         load(sb, t_begin + 1);
         __syncthreads();  // the resident weights
+        unsigned long long tc[3] = {0, 0, 0}, tm0 = 0, t_all = FB_DG ? fb_clk() : 0;
+        auto stamp = [&](int k) __attribute__((always_inline)) {
+            if (FB_DG) {
+                const unsigned long long t1 = fb_clk();
+                tc[k] += t1 - tm0;
+                tm0 = t1;
+            }
+        };
         for (int i = 0; i < ntile; i += 2) {  // as k_bwd_fused32: an even number of iterations
+            if (FB_DG) tm0 = fb_clk();
             store(sa, 0);
+            stamp(0);
             load(sa, t_begin + i + 2);
+            stamp(1);
             __syncthreads();
+            stamp(2);
             store(sb, 1);
+            stamp(0);
             load(sb, t_begin + i + 3);
+            stamp(1);
             __syncthreads();
+            stamp(2);
+        }
+        if (FB_DG && p.dbg && lane == 0) {
+            unsigned long long* d = p.dbg + ((size_t)bid * 8 + 4 + wid) * 8;
+            d[0] = tc[0];
+            d[1] = tc[1];
+            d[2] = tc[2];
+            d[3] = 0;
+            d[4] = fb_clk() - t_all;
+            d[5] = ntile;
         }
         __syncthreads();  // the final reductions (MFMA waves)
         return;
@@ -686,14 +714,26 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
             __builtin_amdgcn_raw_buffer_store_b128(data, rd, (unsigned)(h * p.W + w) * 64u + (unsigned)j * 16u, 0, 2);
         }
     };
+    unsigned long long tc[4] = {0, 0, 0, 0}, t0 = 0, t_all = FB_DG ? fb_clk() : 0;
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+        if (FB_DG) {
+            const unsigned long long t1 = fb_clk();
+            tc[k] += t1 - t0;
+            t0 = t1;
+        }
+    };
     f32x16 accp0, accp1;
-    for (int it = 0; it < ntile; ++it) {
+    auto tile = [&](int it, auto EPI) __attribute__((always_inline)) {  // as k_bwd_fused32's: branch-free, first peeled
+        if (FB_DG) t0 = fb_clk();
         __syncthreads();  // tile it is in buffer it & 1
+        stamp(0);
         const __bf16* dyh = smem + (it & 1) * FD_BUF;
         const __bf16* xsrc = dyh + FB_DYH + hh * FB_XH;
-        // ---- weight gradient: one 16-pixel row per k-step, 4 taps of this wave's x half (+ tap 8 on 4 rows)
+        // ---- weight gradient: one 16-pixel row per k-step, 4 taps of this wave's x half (+ tap 8 on its 4 rows,
+        // first); tile it - 1's two epilogue halves between the rows
 #pragma unroll
-        for (int r = 0; r < FB_TH; ++r) {
+        for (int rr = 0; rr < FB_TH; ++rr) {
+            const int r = (4 * tg + rr) & (FB_TH - 1);
             const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + pk) * FB_DL + ch16;
             const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
             const __bf16* xr = xsrc + (r * FB_HW + pk) * FB_XL + ch16;
@@ -702,15 +742,16 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
                 const bf16x8 bfr = tr_pair(xr + toffx[j], xr + toffx[j] + 8 * FB_XL);
                 accw[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, accw[j], 0, 0, 0);
             }
-            if ((r >> 2) == tg) {
+            if (rr < 4) {
                 const __bf16* x8 = xr + (2 * FB_HW + 2) * FB_XL;
                 accw[4] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_pair(x8, x8 + 8 * FB_XL), accw[4], 0, 0, 0);
             }
+            if constexpr (decltype(EPI)::v) {
+                if (rr == 1) epilogue(accp0, p.du, true, t_begin + it - 1);
+                if (rr == 5) epilogue(accp1, p.dsk, false, t_begin + it - 1);
+            }
         }
-        if (it > 0) {
-            epilogue(accp0, p.du, true, t_begin + it - 1);
-            epilogue(accp1, p.dsk, false, t_begin + it - 1);
-        }
+        stamp(1);
         // ---- dgrad of tile pixels 32 wid ..: C^T[ci][px], ci halves up / skip
         f32x16 accd0, accd1;
 #pragma unroll
@@ -733,6 +774,17 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
         }
         accp0 = accd0;
         accp1 = accd1;
+        stamp(2);
+    };
+    if (ntile > 0) tile(0, BoolC<false>{});
+    for (int it = 1; it < ntile; ++it) tile(it, BoolC<true>{});
+    if (FB_DG && p.dbg && lane == 0) {
+        unsigned long long* d = p.dbg + ((size_t)bid * 8 + wid) * 8;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = tc[k];
+        d[4] = d[5] = 0;
+        d[6] = fb_clk() - t_all;
+        d[7] = ntile;
     }
     if (ntile > 0) {
         epilogue(accp0, p.du, true, t_begin + ntile - 1);
@@ -872,6 +924,7 @@ extern "C" int sd_conv3x3_bwd_fused_dec(const void* da, const void* y, const flo
     p.dsk = (__bf16*)dskip;
     p.slab = slab;
     p.part = reinterpret_cast<float2*>(partials);
+    p.dbg = FB_DG ? sd_debug_ptr() : nullptr;
     hipLaunchKernelGGL(k_bwd_fused_dec, dim3(blocks), dim3(512), 0, to_stream(s), p);
     return sd_check_launch("sd_conv3x3_bwd_fused_dec");
 }
