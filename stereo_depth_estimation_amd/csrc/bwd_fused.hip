@@ -57,7 +57,7 @@ struct BwdArgs {
     const float *psc, *psh, *pmu, *pis;               // the previous BatchNorm layer (x = relu(psc*yp + psh))
     const __bf16* wd;                                 // dgrad-packed weights [32 ci][kpad], k = tap*32 + co (flipped)
     int kpad;
-    int B, H, W, tiles_x, tiles_y, ntiles, tps;       // tps: tiles per block (its split-K range)
+    int B, H, W, tiles_x, tiles_y;                    // tiles per block: fb_ntile (its split-K range)
     __bf16* dx;                                       // [B*H*W][32]
     float* slab;                                      // [blocks][32 co][288], k = tap*32 + ci
     float2* part;                                     // [blocks][32] (sum dz, sum dz*xhat) of the previous layer
@@ -71,14 +71,20 @@ __device__ __forceinline__ int fb_pixel(int item) { return (item / (8 * PPX)) * 
 template <int PPX>
 __device__ __forceinline__ int fb_piece(int item) { return (item >> 3) % PPX; }
 
-// tile index -> (column strip tx, tile row ty, image b), ty fastest: a block walks down a 32-pixel column strip, so
-// the two halo rows a tile shares with the one above were loaded one tile earlier and are L2 hits (row-major order
-// re-fetched them from beyond L2 one tile row = 10 tiles later: 1.5x the algorithmic reads, PMC)
-__device__ __forceinline__ void fb_tile(const BwdArgs& p, int tl, int& tx, int& ty, int& b) {
-    ty = tl % p.tiles_y;
-    const int r = tl / p.tiles_y;
-    tx = r % p.tiles_x;
-    b = r / p.tiles_x;
+// A block's k-th tile -> (column strip tx, tile row ty, image b). Blocks own whole 16-pixel column strips (strip
+// bid, bid + nblk, ...) and walk down each, ty fastest: the two halo rows a tile shares with the one above were
+// loaded one tile earlier (L2 hits), and the blocks of one XCD (consecutive bid) walk adjacent strips side by side,
+// so the halo columns two strips share are fetched once for both (row-major order re-fetched the shared rows from
+// beyond L2: 1.5x the algorithmic reads; one contiguous strip range per block: 1.24x, PMC)
+__device__ __forceinline__ void fb_tile(int tiles_x, int tiles_y, int bid, int nblk, int k, int& tx, int& ty, int& b) {
+    const int strip = bid + (k / tiles_y) * nblk;
+    ty = k % tiles_y;
+    tx = strip % tiles_x;
+    b = strip / tiles_x;
+}
+__device__ __forceinline__ int fb_ntile(int tiles_x, int tiles_y, int B, int bid, int nblk) {
+    const int nstrips = tiles_x * B;
+    return bid < nstrips ? ((nstrips - 1 - bid) / nblk + 1) * tiles_y : 0;
 }
 
 __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
@@ -92,8 +98,8 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
     const int wid = (tid >> 6) & 3;
     // XCD-contiguous block numbering: the tile ranges of one XCD's blocks are neighbours (shared halo rows in its L2)
     const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    const int t_begin = bid * p.tps;
-    const int ntile = max(0, min(p.ntiles, t_begin + p.tps) - t_begin);
+    const int t_begin = 0;  // tiles are numbered per block (fb_tile)
+    const int ntile = fb_ntile(p.tiles_x, p.tiles_y, p.B, bid, gridDim.x);
     const int hw = p.H * p.W;
 
     // the dgrad weights, resident for the launch (all threads; before the first barrier)
@@ -152,7 +158,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             const bool live = tile < t_begin + ntile;
             const int tl = live ? tile : t_begin;
             int tx, ty, b;
-            fb_tile(p, tl, tx, ty, b);
+            fb_tile(p.tiles_x, p.tiles_y, bid, gridDim.x, tl, tx, ty, b);
             const int h0 = ty * FB_TH - 1, w0 = tx * FB_TW - 1;
             const size_t img = (size_t)b * hw * 32;
             const __amdgpu_buffer_rsrc_t ra =
@@ -327,7 +333,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
         }
         asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see the writes above
         int tx, ty, b;
-        fb_tile(p, tl, tx, ty, b);
+        fb_tile(p.tiles_x, p.tiles_y, bid, gridDim.x, tl, tx, ty, b);
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(p.dx + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
         uint4 vv[2];
@@ -477,7 +483,7 @@ struct DecArgs {
     const float *ssc, *ssh;                 // the skip layer's forward affine (x_skip = relu(ssc*xs + ssh))
     const __bf16* wd;                       // dgrad-packed weights [64 ci][kpad], k = tap*32 + co (flipped)
     int kpad;
-    int B, H, W, tiles_x, tiles_y, ntiles, tps;
+    int B, H, W, tiles_x, tiles_y;
     __bf16 *du, *dsk;                       // [B*H*W][32] each
     float* slab;                            // [blocks][32 co][576], k = tap*64 + ci
     float2* part;                           // [blocks][32]: (sum d(up), 0) per channel
@@ -495,14 +501,11 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
     const bool is_loader = tid >= 256;
     const int wid = (tid >> 6) & 3;
     const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tile ranges
-    const int t_begin = bid * p.tps;
-    const int ntile = max(0, min(p.ntiles, t_begin + p.tps) - t_begin);
+    const int t_begin = 0;  // tiles are numbered per block (fb_tile)
+    const int ntile = fb_ntile(p.tiles_x, p.tiles_y, p.B, bid, gridDim.x);
     const int hw = p.H * p.W;
     auto tile_of = [&](int tl, int& tx, int& ty, int& b) __attribute__((always_inline)) {
-        ty = tl % p.tiles_y;
-        const int r = tl / p.tiles_y;
-        tx = r % p.tiles_x;
-        b = r / p.tiles_x;
+        fb_tile(p.tiles_x, p.tiles_y, bid, gridDim.x, tl, tx, ty, b);
     };
 
     for (int i = tid; i < 64 * 36; i += 512) {  // the dgrad weights, resident for the launch
@@ -834,8 +837,8 @@ extern "C" int sd_conv3x3_bwd_fused_ok(int C, int Cx, int H, int W) {
 }
 
 extern "C" int sd_conv3x3_bwd_fused_splits(int batch, int H, int W) {
-    const long long nt = (long long)batch * (H / FB_TH) * (W / FB_TW);
-    return nt < FB_BLOCKS ? (int)((nt + 7) / 8 * 8) : FB_BLOCKS;
+    const long long ns = (long long)batch * (W / FB_TW);  // column strips: the blocks' unit of work (fb_tile)
+    return ns < FB_BLOCKS ? (int)((ns + 7) / 8 * 8) : FB_BLOCKS;
 }
 
 extern "C" int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* scale, const float* shift,
@@ -870,9 +873,7 @@ extern "C" int sd_conv3x3_bwd_fused(const void* da, const void* y, const float* 
     p.tiles_y = H / FB_TH;
     const long long nt = (long long)batch * p.tiles_x * p.tiles_y;
     SD_REQUIRE(nt < (1LL << 30), "sd_conv3x3_bwd_fused: too many tiles");
-    p.ntiles = (int)nt;
     const int blocks = sd_conv3x3_bwd_fused_splits(batch, H, W);
-    p.tps = (int)((nt + blocks - 1) / blocks);
     p.dx = (__bf16*)dx;
     p.slab = slab;
     p.part = reinterpret_cast<float2*>(partials);
@@ -917,9 +918,7 @@ extern "C" int sd_conv3x3_bwd_fused_dec(const void* da, const void* y, const flo
     p.tiles_y = H / FB_TH;
     const long long nt = (long long)batch * p.tiles_x * p.tiles_y;
     SD_REQUIRE(nt < (1LL << 30), "sd_conv3x3_bwd_fused_dec: too many tiles");
-    p.ntiles = (int)nt;
     const int blocks = sd_conv3x3_bwd_fused_splits(batch, H, W);
-    p.tps = (int)((nt + blocks - 1) / blocks);
     p.du = (__bf16*)du;
     p.dsk = (__bf16*)dskip;
     p.slab = slab;
