@@ -189,51 +189,6 @@ __device__ __forceinline__ void wg_store(float* dw, long long e, float v, int N,
     }
 }
 
-// G = 1 with WRED_U output quads per thread: each quad sums its splits into accumulator (split % 4) in increasing
-// split order, as wgrad_reduce_body<1> (bit-identical), with the U quads' loads in flight together (4U per lane
-// instead of 4) and U times fewer blocks (deep layers: 4-16 splits over 0.1-0.6 M quads)
-constexpr int WRED_U = 4;
-__device__ __forceinline__ void wgrad_reduce_g1(const float* __restrict__ slab, int splits, long long total4, int N,
-                                                int layout, int ci_pad, int ci_real, float* __restrict__ dw, int bid,
-                                                int nblocks) {
-    const float4* s4 = reinterpret_cast<const float4*>(slab);
-    for (long long q0 = (long long)bid * 256 * WRED_U; q0 < total4; q0 += (long long)nblocks * 256 * WRED_U) {
-        float4 acc[WRED_U][4];
-        long long q[WRED_U];
-#pragma unroll
-        for (int u = 0; u < WRED_U; ++u) {
-            q[u] = q0 + threadIdx.x + 256 * u;
-#pragma unroll
-            for (int a = 0; a < 4; ++a) acc[u][a] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        for (int z = 0; z < splits; z += 4) {
-#pragma unroll
-            for (int u = 0; u < WRED_U; ++u) {
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    if (q[u] < total4 && z + a < splits) {
-                        const float4 v = s4[(size_t)(z + a) * total4 + q[u]];
-                        acc[u][a].x += v.x;
-                        acc[u][a].y += v.y;
-                        acc[u][a].z += v.z;
-                        acc[u][a].w += v.w;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < WRED_U; ++u) {
-            if (q[u] >= total4) continue;
-            const float4* a4 = acc[u];
-            const long long e = 4 * q[u];
-            wg_store(dw, e, (a4[0].x + a4[1].x) + (a4[2].x + a4[3].x), N, layout, ci_pad, ci_real);
-            wg_store(dw, e + 1, (a4[0].y + a4[1].y) + (a4[2].y + a4[3].y), N, layout, ci_pad, ci_real);
-            wg_store(dw, e + 2, (a4[0].z + a4[1].z) + (a4[2].z + a4[3].z), N, layout, ci_pad, ci_real);
-            wg_store(dw, e + 3, (a4[0].w + a4[1].w) + (a4[2].w + a4[3].w), N, layout, ci_pad, ci_real);
-        }
-    }
-}
-
 // G split groups per block (8 or 32), 256 / G float4 outputs per block, 4 independent accumulators per lane: each
 // output quad sums its splits in a fixed order (deterministic for a given split count and G). Small layers have
 // few output quads and many splits (up to 512): G = 32 keeps 16 loads per output in flight instead of 4 (the
@@ -315,11 +270,8 @@ template <int G>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ slab, int splits, int M, int N,
                                                       int layout, int ci_pad, int ci_real, float* __restrict__ dw) {
     __shared__ float4 part[256];
-    if constexpr (G == 1)
-        wgrad_reduce_g1(slab, splits, (long long)M * N / 4, N, layout, ci_pad, ci_real, dw, blockIdx.x, gridDim.x);
-    else
-        wgrad_reduce_body<G>(slab, splits, (long long)M * N / 4, N, layout, ci_pad, ci_real, dw, blockIdx.x,
-                             gridDim.x, part);
+    wgrad_reduce_body<G>(slab, splits, (long long)M * N / 4, N, layout, ci_pad, ci_real, dw, blockIdx.x, gridDim.x,
+                         part);
 }
 
 // Many weight gradients' slab reduces in ONE launch (sd_wgrad_reduce_batch): job j owns blocks [b0, b0 + nblk) and
@@ -350,7 +302,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_batch(const WRedBatch b) {
     else if (j.g == 4)
         wgrad_reduce_body<4>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
     else
-        wgrad_reduce_g1(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk);
+        wgrad_reduce_body<1>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
 }
 
 }  // namespace
@@ -485,7 +437,7 @@ static int wred_plan(const float* slab, int splits, int M, int N, int layout, in
     // where the splits are few (deep layers: 4-64 splits over up to 0.6 M output quads), so that no thread idles and
     // the blocks stream whole 4-KB rows of each slab instead of summing 32 quads through LDS
     g = g_env ? g_env : ((total4 + 31) / 32 < 512 && splits >= 64 ? 32 : splits <= 16 ? 1 : splits <= 64 ? 4 : 8);
-    const int qb = g == 1 ? 256 * WRED_U : 256 / g;  // output quads per block
+    const int qb = 256 / g;
     const long long nb = (total4 + qb - 1) / qb;
     blocks = (int)(nb > 8192 ? 8192 : nb);
     return 0;
