@@ -32,13 +32,15 @@ constexpr int FB_NI = (FB_HPX * 4 + 255) / 256;    // loader items per thread (3
 constexpr int FB_HSL = (FB_NI * 256 / 32) * 8;     // halo pixel slots (items past the halo land in slots >= FB_HPX)
 static_assert(FB_TH * FB_TW == 128 && FB_TW % 16 == 0, "4 MFMA waves x 32 pixels; tr_pair rows p, p + 8 in one row");
 constexpr int FB_DL = 40;                          // dy halo pixel pitch (80 B: odd 16-B slot count, b128 reads)
-#ifndef FB_XL_P
-#define FB_XL_P 48
-#endif
-constexpr int FB_XL = FB_XL_P;                     // x halo pixel pitch
+constexpr int FB_XL = 48;                          // x halo pixel pitch (96 B)
+// x halo: channels 16..31 of pixel p sit FB_XC elements after its channels 0..15 (past the next pixel's first half):
+// the transposed reads of a 32-lane half (4 pixels x channels {0..15, 16..31}) then cover the 64 banks once, where the
+// plain +16 layout put pixel 3's first half on pixel 0's second (2-way conflicts, PMC 0.37 extra cycles per access)
+constexpr int FB_XC = 64;
+__device__ __forceinline__ int fb_xoff(int c) { return (c & 15) + (c >> 4) * FB_XC; }  // channel c's element offset
 constexpr int FB_WL = 9 * 32 + 8;                  // dgrad weight row (592 B, odd slot count)
 constexpr int FB_SL = 40;                          // raw y_prev stash pitch (the sums' operand)
-constexpr int FB_DYH = FB_HSL * FB_DL, FB_XH = FB_HSL * FB_XL, FB_ST = FB_TH * FB_TW * FB_SL;
+constexpr int FB_DYH = FB_HSL * FB_DL, FB_XH = FB_HSL * FB_XL + (FB_XC - FB_XL + 16), FB_ST = FB_TH * FB_TW * FB_SL;
 constexpr int FB_BUF = FB_DYH + FB_XH + FB_ST;     // elements per LDS buffer
 constexpr int FB_BLOCKS = 256;                     // one per CU
 #ifndef FB_EXP
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
                         x = ok ? x : make_uint4(0, 0, 0, 0);
                     }
                     *reinterpret_cast<uint4*>(dyh + px * FB_DL + piece * 8) = d;
-                    *reinterpret_cast<uint4*>(xh + px * FB_XL + piece * 8) = x;
+                    *reinterpret_cast<uint4*>(xh + px * FB_XL + fb_xoff(piece * 8)) = x;
                     if (stash[i] >= 0) *reinterpret_cast<uint4*>(st + stash[i]) = q.x[i];  // raw y_prev (0 outside)
                 }
             };
@@ -370,7 +372,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused32(const BwdArgs p) {
             const int r = (2 * wid + rr) & (FB_TH - 1);
             const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + pk) * FB_DL + ch16;  // dy^T of row r
             const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
-            const __bf16* xr = xh + (r * FB_HW + pk) * FB_XL + ch16;
+            const __bf16* xr = xh + (r * FB_HW + pk) * FB_XL + fb_xoff(ch16);
             const bf16x8 b0 = tr_pair(xr + toffx0, xr + toffx0 + 8 * FB_XL);
             const bf16x8 b1 = tr_pair(xr + toffx1, xr + toffx1 + 8 * FB_XL);
             accw[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, accw[0], 0, 0, 0);
@@ -603,8 +605,8 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
                         xu = ok ? xu : make_uint4(0, 0, 0, 0);
                     }
                     *reinterpret_cast<uint4*>(dyh + px * FB_DL + piece * 8) = d;
-                    *reinterpret_cast<uint4*>(xuh + px * FB_XL + piece * 8) = xu;
-                    *reinterpret_cast<uint4*>(xsh + px * FB_XL + piece * 8) = xs;
+                    *reinterpret_cast<uint4*>(xuh + px * FB_XL + fb_xoff(piece * 8)) = xu;
+                    *reinterpret_cast<uint4*>(xsh + px * FB_XL + fb_xoff(piece * 8)) = xs;
                 }
             };
             if (q.edge)
@@ -739,7 +741,7 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
             const int r = (4 * tg + rr) & (FB_TH - 1);
             const __bf16* a0 = dyh + ((r + 1) * FB_HW + 1 + pk) * FB_DL + ch16;
             const bf16x8 af = tr_pair(a0, a0 + 8 * FB_DL);
-            const __bf16* xr = xsrc + (r * FB_HW + pk) * FB_XL + ch16;
+            const __bf16* xr = xsrc + (r * FB_HW + pk) * FB_XL + fb_xoff(ch16);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const bf16x8 bfr = tr_pair(xr + toffx[j], xr + toffx[j] + 8 * FB_XL);
