@@ -94,9 +94,6 @@ class GemmTimer:
         if name == "sd_conv3x3_bwd_fused_dec":  # the same for dec1.0 (64 -> 32 channels)
             B, H, W = args[13:16]
             return 2.0 * 2.0 * B * H * W * 32 * 9 * 64, "k_bwd_fused_dec"
-        if name == "sd_conv3x3_fwd_fused":  # training forward of a full-resolution 32 / 64 -> 32 conv + BN stats
-            cin, (B, H, W) = args[0], args[9:12]
-            return 2.0 * B * H * W * 32 * 9 * cin, f"k_fwd_fused<{cin}>"
         xin = eng.ws.t["xin"].data_ptr()
         if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             dt, src, B, H, W, _, N = args[:7]
@@ -119,7 +116,7 @@ class GemmTimer:
 
     def __call__(self, name, args, phase):
         if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd",
-                        "sd_conv3x3_bwd_fused", "sd_conv3x3_bwd_fused_dec", "sd_conv3x3_fwd_fused"):
+                        "sd_conv3x3_bwd_fused", "sd_conv3x3_bwd_fused_dec"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
         ev.record(self._stream(args[-1]))  # the launch stream (SD_SIDE_REDUCE=2 puts some GEMMs on a second one)
@@ -135,15 +132,11 @@ class GemmTimer:
                 nbytes = 4.0 * args[14] * args[15] * args[16] * 32 * 2
             if name == "sd_conv3x3_bwd_fused_dec":  # da, y, u, y_skip read, d(u), d(skip) written once
                 nbytes = 6.0 * args[13] * args[14] * args[15] * 32 * 2
-            if name == "sd_conv3x3_fwd_fused":  # x read and y written once (bf16) + the weights
-                P = args[9] * args[10] * args[11]
-                nbytes = 2.0 * (P * args[0] + P * 32 + 9 * args[0] * 32)
             self.pending.append((kname, flops, start, ev, name, self._shape(name, args), nbytes))
-            fwd3 = (name == "sd_conv_gemm" and args[1].taps == 9) or name == "sd_conv3x3_fwd_fused"
-            if fwd3 and self._last_phase == "fwd":
+            if name == "sd_conv_gemm" and self._last_phase == "fwd":
                 # forward order (model.py:79-104): the first 10 3x3 convs are enc1..enc4, bottleneck
-                if self._fwd_conv < 10:
-                    self.encoder.append((self._fwd_conv, flops, nbytes, start, ev))
+                if self._fwd_conv < 10 and args[1].taps == 9:
+                    self.encoder.append((self._fwd_conv, flops, self._min_bytes(args), start, ev))
                     self._fwd_conv += 1
 
     def _min_bytes(self, args):
@@ -196,8 +189,6 @@ class GemmTimer:
             return f"bwd_fused P={args[14] * args[15] * args[16]} C=32"
         if name == "sd_conv3x3_bwd_fused_dec":
             return f"bwd_fused_dec P={args[13] * args[14] * args[15]} C=64->32"
-        if name == "sd_conv3x3_fwd_fused":
-            return f"fwd_fused P={args[9] * args[10] * args[11]} C={args[0]}->32"
         if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             s = args[1]
             return f"fwd M={args[2] * args[3] * args[4]} N={args[6]} K={s.taps}x{s.chans[0] + s.chans[1]}"

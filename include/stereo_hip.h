@@ -355,16 +355,6 @@ int sd_conv3x3_bwd_fused_dec(const void* da, const void* y, const float* scale, 
                              const float* sscale, const float* sshift, const void* wd, int kpad, int batch, int H,
                              int W, void* du, void* dskip, float* slab, float* partials, sd_stream s);
 
-/* Forward of the same full-resolution layers with their BatchNorm statistics (model.py:36-41, training): y =
- * conv3x3(x) stored bf16, x = relu(scale0*x0 + shift0) (scale0/shift0 NULL: x0 raw), or for cin = 64
- * cat(that, relu(scale1*x1 + shift1)) (dec1.0: x0 = the ConvTranspose2d output u, raw; x1 = the skip's raw output);
- * w: sd_pack_conv3_w forward layout [32][kpad], k = tap*cin + ci; partials[splits][32] float2 (sum, sumsq) of the
- * stored values, splits = sd_conv3x3_bwd_fused_splits(batch, H, W), for sd_bn_fwd_finalize. */
-int sd_conv3x3_fwd_fused_ok(int Cin, int C, int H, int W);
-int sd_conv3x3_fwd_fused(int cin, const void* x0, const float* scale0, const float* shift0, const void* x1,
-                         const float* scale1, const float* shift1, const void* w, int kpad, int batch, int H, int W,
-                         void* y, float* partials, sd_stream s);
-
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----
  * One flat fp32 parameter/gradient/state buffer (all tensors share lr/betas/eps/wd).
  * The step is skipped (and *step not advanced) when *count == 0 (train.py:331-332). */

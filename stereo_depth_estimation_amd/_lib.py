@@ -113,8 +113,6 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_conv3x3_bwd_fused_splits": (_i, [_i, _i, _i]),
     "sd_conv3x3_bwd_fused": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]),
     "sd_conv3x3_bwd_fused_dec_ok": (_i, [_i, _i, _i, _i, _i]),
-    "sd_conv3x3_fwd_fused_ok": (_i, [_i, _i, _i, _i]),
-    "sd_conv3x3_fwd_fused": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]),
     "sd_conv3x3_bwd_fused_dec": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p,
                                       _p]),
     "sd_last_error": (ctypes.c_char_p, []),

@@ -828,256 +828,6 @@ __global__ __launch_bounds__(512) void k_bwd_fused_dec(const DecArgs p) {
             make_float2((redf[tid] + redf[32 + tid]) + (redf[64 + tid] + redf[96 + tid]), 0.f);
 }
 
-
-// =====================================================================================================================
-// Forward of a full-resolution conv + BatchNorm statistics in the fused kernels' layout (model.py:36-41: enc1.1, dec1.1
-// with CX = 32 input channels x = relu(bn(y_prev)); dec1.0 with CX = 64, x = cat(u, relu(bn(y_skip)))): y = conv(x)
-// stored bf16 and the per-channel (sum, sumsq) of the stored values as one partial row per block, for
-// sd_bn_fwd_finalize. Same block structure as k_bwd_fused32: 4 loader waves stage the BN+ReLU'd x halo of 8x16 tiles
-// (column strips, interleaved over an XCD's blocks) into an LDS double buffer; 4 MFMA waves compute 32 pixels x 32
-// output channels each (v_mfma_f32_32x32x16_bf16, weights resident in LDS), the epilogue of a tile software-pipelined
-// behind the next tile's MFMAs.
-struct FwdFArgs {
-    const __bf16 *x0, *x1;         // [B*H*W][32]: the first source (raw), the second (CX = 64: the skip's raw y)
-    const float *s0, *h0, *s1, *h1;  // BN affines of the sources (s0 == nullptr: source 0 raw, as u)
-    const __bf16* w;               // forward-packed weights [32 co][kpad], k = tap*CX + ci
-    int kpad;
-    int B, H, W, tiles_x, tiles_y;
-    __bf16* y;                     // [B*H*W][32]
-    float2* part;                  // [blocks][32]: (sum, sumsq) of the stored values
-};
-constexpr int FF_XL = 40;  // x halo pitch (80 B: odd 16-B slot count, conflict-free b128 reads at any tap offset)
-
-template <int CX>
-__global__ __launch_bounds__(512) void k_fwd_fused(const FwdFArgs p) {
-    constexpr int NS = CX / 32;                 // 32-channel sources
-    constexpr int XH = FB_HSL * FF_XL;          // one source's halo
-    constexpr int BUF = NS * XH;
-    constexpr int WL = 9 * CX + 8;              // weight row (odd 16-B slot count)
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
-    __shared__ __attribute__((aligned(16))) __bf16 wls[32 * WL];
-    __shared__ __attribute__((aligned(16))) __bf16 scr[4 * 32 * 32];
-    __shared__ __attribute__((aligned(16))) float redf[4 * 32 * 2];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const bool is_loader = tid >= 256;
-    const int wid = (tid >> 6) & 3;
-    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    const int ntile = fb_ntile(p.tiles_x, p.tiles_y, p.B, bid, gridDim.x);
-    const int hw = p.H * p.W;
-
-    for (int i = tid; i < 32 * (9 * CX / 8); i += 512) {  // the weights, resident for the launch
-        const int r = i / (9 * CX / 8), c8 = i - r * (9 * CX / 8);
-        *reinterpret_cast<uint4*>(wls + r * WL + c8 * 8) =
-            *reinterpret_cast<const uint4*>(p.w + (size_t)r * p.kpad + c8 * 8);
-    }
-
-    if (is_loader) {
-        // =========================================================== loader waves
-        const int ltid = tid - 256;
-        const int piece = fb_piece<4>(ltid);
-        constexpr unsigned OOB = 0x80000000u;
-        float4 a0 = {1.f, 1.f, 1.f, 1.f}, a1 = a0, b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0, c0 = a0, c1 = a0, d0 = b0,
-               d1 = b0;
-        const bool raw0 = p.s0 == nullptr;
-        if (!raw0) {
-            a0 = *reinterpret_cast<const float4*>(p.s0 + piece * 8);
-            a1 = *reinterpret_cast<const float4*>(p.s0 + piece * 8 + 4);
-            b0 = *reinterpret_cast<const float4*>(p.h0 + piece * 8);
-            b1 = *reinterpret_cast<const float4*>(p.h0 + piece * 8 + 4);
-        }
-        if (NS == 2) {
-            c0 = *reinterpret_cast<const float4*>(p.s1 + piece * 8);
-            c1 = *reinterpret_cast<const float4*>(p.s1 + piece * 8 + 4);
-            d0 = *reinterpret_cast<const float4*>(p.h1 + piece * 8);
-            d1 = *reinterpret_cast<const float4*>(p.h1 + piece * 8 + 4);
-        }
-        unsigned geo[FB_NI];
-#pragma unroll
-        for (int i = 0; i < FB_NI; ++i) {
-            const int px = fb_pixel<4>(ltid + 256 * i);
-            const int hy = px / FB_HW, hx = px - hy * FB_HW;
-            geo[i] = px < FB_HPX ? (unsigned)(hy << 8 | hx) : 0xffffffffu;
-        }
-        const bool w3 = (ltid & ~63) + 256 * (FB_NI - 1) < FB_HPX * 4;
-        unsigned need = 0;
-#pragma unroll
-        for (int i = 0; i < FB_NI; ++i) need |= (unsigned)(geo[i] != 0xffffffffu) << i;
-        struct Set {
-            uint4 v[NS][FB_NI];
-            unsigned m;
-            bool edge;
-        };
-        Set sa, sb;
-        auto load = [&](Set& q, int k) __attribute__((always_inline)) {
-            const bool live = k < ntile;
-            int tx, ty, b;
-            fb_tile(p.tiles_x, p.tiles_y, bid, gridDim.x, live ? k : 0, tx, ty, b);
-            const int h0 = ty * FB_TH - 1, w0 = tx * FB_TW - 1;
-            const size_t img = (size_t)b * hw * 32;
-            __amdgpu_buffer_rsrc_t rs[NS];
-            rs[0] = __builtin_amdgcn_make_buffer_rsrc((void*)(p.x0 + img), (short)0, hw * 64, 0x00020000);
-            if (NS == 2) rs[NS - 1] = __builtin_amdgcn_make_buffer_rsrc((void*)(p.x1 + img), (short)0, hw * 64, 0x00020000);
-            unsigned m = 0;
-#pragma unroll
-            for (int i = 0; i < FB_NI; ++i) {
-                if (i == FB_NI - 1 && !w3) break;
-                const int h = h0 + (int)(geo[i] >> 8), w = w0 + (int)(geo[i] & 0xffu);
-                const bool ok = live & (geo[i] != 0xffffffffu) & (h >= 0) & (h < p.H) & (w >= 0) & (w < p.W);
-                m |= (unsigned)ok << i;
-                const unsigned off = ok ? (unsigned)(h * p.W + w) * 64u + (unsigned)piece * 16u : OOB;
-#pragma unroll
-                for (int sidx = 0; sidx < NS; ++sidx) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs[sidx], off, 0, 0);
-                    q.v[sidx][i] = make_uint4(v[0], v[1], v[2], v[3]);
-                }
-            }
-            q.m = m;
-            q.edge = __builtin_amdgcn_ballot_w64(m != (w3 ? need : need & ((1u << (FB_NI - 1)) - 1))) != 0;
-        };
-        auto store = [&](Set& q, int buf) __attribute__((always_inline)) {
-            __bf16* xh = smem + buf * BUF;
-            auto put = [&](auto SEL) __attribute__((always_inline)) {
-#pragma unroll
-                for (int i = 0; i < FB_NI; ++i) {
-                    if (i == FB_NI - 1 && !w3) break;
-                    const bool ok = (q.m >> i) & 1u;
-                    const int px = fb_pixel<4>(ltid + 256 * i);
-                    uint4 x0 = raw0 ? q.v[0][i] : bnrelu_pk(q.v[0][i], a0, a1, b0, b1);
-                    if constexpr (decltype(SEL)::v) x0 = ok ? x0 : make_uint4(0, 0, 0, 0);  // zero padding
-                    *reinterpret_cast<uint4*>(xh + px * FF_XL + piece * 8) = x0;
-                    if constexpr (NS == 2) {
-                        uint4 x1 = bnrelu_pk(q.v[NS - 1][i], c0, c1, d0, d1);
-                        if constexpr (decltype(SEL)::v) x1 = ok ? x1 : make_uint4(0, 0, 0, 0);
-                        *reinterpret_cast<uint4*>(xh + XH + px * FF_XL + piece * 8) = x1;
-                    }
-                }
-            };
-            if (q.edge)
-                put(BoolC<true>{});
-            else
-                put(BoolC<false>{});
-        };
-        load(sa, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        load(sb, 1);
-        __syncthreads();  // the resident weights
-        for (int i = 0; i < ntile; i += 2) {
-            store(sa, 0);
-            load(sa, i + 2);
-            __syncthreads();
-            store(sb, 1);
-            load(sb, i + 3);
-            __syncthreads();
-        }
-        __syncthreads();  // the statistics reduction (MFMA waves)
-        return;
-    }
-
-    // =============================================================== MFMA waves
-    __syncthreads();  // the resident weights
-    float own[16];  // (sum, sumsq) of this lane's 8 channels (lane % 4), stats_add layout as bns_add's
-#pragma unroll
-    for (int j = 0; j < 16; ++j) own[j] = 0.f;
-    __bf16* const scw = scr + wid * 32 * 32;
-    auto swz = [](int j, int px) { return j ^ ((px >> 1) & 3); };
-    auto epilogue = [&](const f32x16& acc, int k) __attribute__((always_inline)) {
-        uint2 pk2[4];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            bf16x4 v;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = (__bf16)acc[4 * g4 + q];
-            pk2[g4] = *reinterpret_cast<uint2*>(&v);
-        }
-#pragma unroll
-        for (int kq = 0; kq < 4; kq += 2) {
-            const auto rx = __builtin_amdgcn_permlane32_swap(pk2[kq].x, pk2[kq + 1].x, false, false);
-            const auto ry = __builtin_amdgcn_permlane32_swap(pk2[kq].y, pk2[kq + 1].y, false, false);
-            const int px = lane & 31, j = kq + (lane >> 5);
-            *reinterpret_cast<uint4*>(scw + px * 32 + swz(j, px) * 8) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-        }
-        asm volatile("" ::: "memory");
-        int tx, ty, b;
-        fb_tile(p.tiles_x, p.tiles_y, bid, gridDim.x, k, tx, ty, b);
-        const __amdgpu_buffer_rsrc_t rd =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + (size_t)b * hw * 32), (short)0, hw * 64, 0x00020000);
-        uint4 vv[2];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const int px = rr * 16 + (lane >> 2), j = lane & 3;
-            vv[rr] = *reinterpret_cast<const uint4*>(scw + px * 32 + swz(j, px) * 8);
-        }
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const int q = wid * 32 + rr * 16 + (lane >> 2), j = lane & 3;
-            const int h = ty * FB_TH + q / FB_TW, w = tx * FB_TW + q % FB_TW;
-            const unsigned wv[4] = {vv[rr].x, vv[rr].y, vv[rr].z, vv[rr].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {  // channel pair e: own[4e + {0, 1}] sums, [4e + {2, 3}] sums of squares
-                const float lo = __uint_as_float(wv[e] << 16), hi = __uint_as_float(wv[e] & 0xffff0000u);
-                own[4 * e] += lo;
-                own[4 * e + 1] += hi;
-                own[4 * e + 2] = __builtin_fmaf(lo, lo, own[4 * e + 2]);
-                own[4 * e + 3] = __builtin_fmaf(hi, hi, own[4 * e + 3]);
-            }
-            __attribute__((ext_vector_type(4))) unsigned data = {vv[rr].x, vv[rr].y, vv[rr].z, vv[rr].w};
-            __builtin_amdgcn_raw_buffer_store_b128(data, rd, (unsigned)(h * p.W + w) * 64u + (unsigned)j * 16u, 0, 2);
-        }
-    };
-    const int c8 = 8 * (lane >> 5);
-    const __bf16* wrow = wls + (lane & 31) * WL + c8;
-    const int qd = wid * 32 + (lane & 31);
-    const int xoff = ((qd / FB_TW) * FB_HW + qd % FB_TW) * FF_XL + c8;
-    f32x16 accp;
-    auto tile = [&](int k, auto EPI) __attribute__((always_inline)) {
-        __syncthreads();  // tile k is in buffer k & 1
-        const __bf16* xh = smem + (k & 1) * BUF;
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        // C[co][px] over 9 taps x CX / 16 k-steps; the previous tile's epilogue after the third tap
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int toff = ((tap / 3) * FB_HW + tap % 3) * FF_XL;
-#pragma unroll
-            for (int kk = 0; kk < CX / 16; ++kk) {
-                const int sidx = kk / 2, k16 = (kk & 1) * 16;
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + tap * CX + kk * 16);
-                const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xh + sidx * XH + xoff + toff + k16);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx, acc, 0, 0, 0);
-            }
-            if constexpr (decltype(EPI)::v)
-                if (tap == 2) epilogue(accp, k - 1);
-        }
-        accp = acc;
-    };
-    if (ntile > 0) tile(0, BoolC<false>{});
-    for (int k = 1; k < ntile; ++k) tile(k, BoolC<true>{});
-    if (ntile > 0) epilogue(accp, ntile - 1);
-    if (ntile & 1) __syncthreads();  // the loaders' last (even-count) iteration
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-#pragma unroll
-        for (int o = 4; o < 64; o <<= 1) own[k] += __shfl_xor(own[k], o);
-    if (lane < 4) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k)  // k: channel k / 2, {sum, sumsq} k & 1
-            redf[(wid * 32 + lane * 8 + k / 2) * 2 + (k & 1)] = own[(k & ~3) | ((k & 1) << 1) | ((k >> 1) & 1)];
-    }
-    __syncthreads();
-    if (tid < 32) {
-        float sm = 0.f, sq = 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            sm += redf[(w * 32 + tid) * 2];
-            sq += redf[(w * 32 + tid) * 2 + 1];
-        }
-        p.part[(size_t)bid * 32 + tid] = make_float2(sm, sq);
-    }
-}
-
 }  // namespace
 
 unsigned long long* sd_debug_ptr();
@@ -1178,41 +928,4 @@ extern "C" int sd_conv3x3_bwd_fused_dec(const void* da, const void* y, const flo
     p.dbg = FB_DG ? sd_debug_ptr() : nullptr;
     hipLaunchKernelGGL(k_bwd_fused_dec, dim3(blocks), dim3(512), 0, to_stream(s), p);
     return sd_check_launch("sd_conv3x3_bwd_fused_dec");
-}
-
-extern "C" int sd_conv3x3_fwd_fused_ok(int Cin, int C, int H, int W) {
-    return (Cin == 32 || Cin == 64) && C == 32 && sd_conv3x3_bwd_fused_ok(32, 32, H, W) == 1 ? 1 : 0;
-}
-
-extern "C" int sd_conv3x3_fwd_fused(int cin, const void* x0, const float* scale0, const float* shift0, const void* x1,
-                                    const float* scale1, const float* shift1, const void* w, int kpad, int batch, int H,
-                                    int W, void* y, float* partials, sd_stream s) {
-    SD_REQUIRE(sd_conv3x3_fwd_fused_ok(cin, 32, H, W) == 1 && batch > 0,
-               "sd_conv3x3_fwd_fused: 32 or 64 -> 32 channels, H %% %d == 0, W %% %d == 0 (got %d, %dx%d)", FB_TH,
-               FB_TW, cin, H, W);
-    SD_REQUIRE(x0 && w && y && partials && kpad >= 9 * cin && (scale0 == nullptr) == (shift0 == nullptr),
-               "sd_conv3x3_fwd_fused: bad args");
-    SD_REQUIRE(cin == 32 ? x1 == nullptr : (x1 && scale1 && shift1), "sd_conv3x3_fwd_fused: sources do not match cin");
-    FwdFArgs p;
-    p.x0 = (const __bf16*)x0;
-    p.x1 = (const __bf16*)x1;
-    p.s0 = scale0;
-    p.h0 = shift0;
-    p.s1 = scale1;
-    p.h1 = shift1;
-    p.w = (const __bf16*)w;
-    p.kpad = kpad;
-    p.B = batch;
-    p.H = H;
-    p.W = W;
-    p.tiles_x = W / FB_TW;
-    p.tiles_y = H / FB_TH;
-    p.y = (__bf16*)y;
-    p.part = reinterpret_cast<float2*>(partials);
-    const int blocks = sd_conv3x3_bwd_fused_splits(batch, H, W);
-    if (cin == 32)
-        hipLaunchKernelGGL(k_fwd_fused<32>, dim3(blocks), dim3(512), 0, to_stream(s), p);
-    else
-        hipLaunchKernelGGL(k_fwd_fused<64>, dim3(blocks), dim3(512), 0, to_stream(s), p);
-    return sd_check_launch("sd_conv3x3_fwd_fused");
 }

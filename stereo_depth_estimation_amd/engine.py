@@ -231,8 +231,6 @@ class UNetEngine:
         # (sd_conv3x3_bwd_fused / _dec: dy stays in LDS; SD_BWD_FUSE=0: weight gradient + dgrad launches;
         # SD_BWD_FUSE=1: the conv1 layers only)
         self.bwd_fuse = {"0": 0, "1": 1}.get(os.environ.get("SD_BWD_FUSE", "2"), 2)
-        # the training forward of the same layers in that layout (sd_conv3x3_fwd_fused; SD_FWD_FUSE=0: the halo conv)
-        self.fwd_fuse = os.environ.get("SD_FWD_FUSE", "1") != "0"
         self._bnsum_rows: dict[str, int] = {}
         # training: the split-K slab reduce of every weight gradient on a second stream (SD_SIDE_REDUCE=1), so it
         # overlaps the next layer's kernels instead of adding a kernel boundary to the critical path; 2: the
@@ -527,26 +525,6 @@ class UNetEngine:
             t["u:" + up.name], up.cout, Hl, Wl, taps=9, src1=t["y:" + sk.name], c1=sk.cout, bn1=self._bn(sk)
         )
 
-    def _fwd_fused_src(self, cl: ConvL):
-        """(x0, scale0, shift0, x1, scale1, shift1) of the fused forward (sd_conv3x3_fwd_fused) for conv `cl`, or None:
-        bf16 training, 32 output channels at a tiling the kernel takes, input relu(bn(conv0)) (a block's conv1) or
-        cat(u, relu(bn(skip))) (a decoder conv0 on 32 + 32 channels)."""
-        ws, t = self.ws, self.ws.t
-        if not (self.fwd_fuse and self.sd_dtype == L.SD_BF16 and cl.cout == 32):
-            return None
-        if L.call("sd_conv3x3_fwd_fused_ok", cl.cin, cl.cout, ws.H >> cl.level, ws.W >> cl.level) != 1:
-            return None
-        if cl.idx == 1:
-            prev = self.convs[cl.blk + ".0"]
-            sc, sh = self._bn(prev)
-            return (t["y:" + prev.name], sc, sh, None, None, None)
-        if cl.blk in UP_OF_DEC:
-            up, sk = self.ups[UP_OF_DEC[cl.blk]], self.convs[SKIP_OF_DEC[cl.blk] + ".1"]
-            if up.cout == 32 and sk.cout == 32:
-                sc, sh = self._bn(sk)
-                return (t["u:" + up.name], None, None, t["y:" + sk.name], sc, sh)
-        return None
-
     def _conv_fwd(self, cl: ConvL, train: bool):
         ws, t, s, dt = self.ws, self.ws.t, self._s(), self.sd_dtype
         Hl, Wl = ws.H >> cl.level, ws.W >> cl.level
@@ -556,21 +534,15 @@ class UNetEngine:
         mean, invstd = t["mean:" + cl.name], t["invstd:" + cl.name]
         scale, shift = t["scale:" + cl.name], t["shift:" + cl.name]
         split = self._use_wsplit(cl, train) and dt == L.SD_BF16
-        fsrc = self._fwd_fused_src(cl) if train else None
         if train:
             stats = t["stats"]
-            if fsrc is not None:  # one pass over x, BN statistics rows from the epilogue
-                x0, s0, h0, x1, s1, h1 = fsrc
-                L.call("sd_conv3x3_fwd_fused", cl.cin, x0.data_ptr(), L.ptr(s0), L.ptr(h0), L.ptr(x1), L.ptr(s1),
-                       L.ptr(h1), self._wp(cl.off_f), cl.kpad_f, ws.B, Hl, Wl, y.data_ptr(), stats.data_ptr(), s)
-            elif split:
+            if split:
                 L.call("sd_conv3x3_ex", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s), cl.cout, cl.kpad_s,
                        L.SD_EPI_STATS, L.SD_CONV_WSPLIT, None, None, y.data_ptr(), stats.data_ptr(), s)
             else:
                 L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STATS,
                        y.data_ptr(), None, 0, None, stats.data_ptr(), s)
-            rows = (L.call("sd_conv3x3_bwd_fused_splits", ws.B, Hl, Wl) if fsrc is not None
-                    else L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cout))
+            rows = L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cout)
             rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
             nbt = self.bufs.get(cl.bn_key + ".num_batches_tracked")
             if self.bn_sync is not None:  # global batch statistics (torch SyncBatchNorm) over the global count
