@@ -95,7 +95,7 @@ class GemmTimer:
             B, H, W = args[13:16]
             return 2.0 * 2.0 * B * H * W * 32 * 9 * 64, "k_bwd_fused_dec"
         xin = eng.ws.t["xin"].data_ptr()
-        if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_conv_gemm_bnfin"):
+        if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             dt, src, B, H, W, _, N = args[:7]
             s = src._obj if hasattr(src, "_obj") else src
             ctot = s.chans[0] + s.chans[1]
@@ -104,8 +104,6 @@ class GemmTimer:
             flops = 2.0 * B * H * W * N * s.taps * ctot
             if name == "sd_conv_gemm_bnsum":  # a dgrad (STORE) that also sums the BatchNorm backward
                 return flops, L.kernel_name("sd_conv_gemm_bnsum_kernel_name", s, H, W, N)
-            if name == "sd_conv_gemm_bnfin":  # a STATS forward whose last block runs the BatchNorm finalize
-                return flops, L.kernel_name("sd_conv_gemm_kernel_name", dt, s, B, H, W, N, L.SD_EPI_STATS)
             return flops, L.kernel_name("sd_conv_gemm_kernel_name", dt, s, B, H, W, N, args[8])
         dt, a, b, B, H, W, M, N = args[:8]
         sb = b._obj if hasattr(b, "_obj") else b
@@ -117,8 +115,8 @@ class GemmTimer:
         return 2.0 * B * H * W * M * n_real, L.kernel_name("sd_wgrad_kernel_name", dt, a, sb, M, N)
 
     def __call__(self, name, args, phase):
-        if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_conv_gemm_bnfin", "sd_wgrad_gemm",
-                        "sd_wgrad_gemm_bnbwd", "sd_conv3x3_bwd_fused", "sd_conv3x3_bwd_fused_dec"):
+        if name not in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_wgrad_gemm", "sd_wgrad_gemm_bnbwd",
+                        "sd_conv3x3_bwd_fused", "sd_conv3x3_bwd_fused_dec"):
             return
         ev = self.torch.cuda.Event(enable_timing=True)
         ev.record(self._stream(args[-1]))  # the launch stream (SD_SIDE_REDUCE=2 puts some GEMMs on a second one)
@@ -129,14 +127,13 @@ class GemmTimer:
                 self._fwd_conv = 0
         else:
             start, flops, kname = self.cur
-            conv = name in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_conv_gemm_bnfin")
-            nbytes = self._min_bytes(args) if conv else 0.0
+            nbytes = self._min_bytes(args) if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum") else 0.0
             if name == "sd_conv3x3_bwd_fused":  # da, y, y_prev read, dx written once (bf16, 32 channels)
                 nbytes = 4.0 * args[14] * args[15] * args[16] * 32 * 2
             if name == "sd_conv3x3_bwd_fused_dec":  # da, y, u, y_skip read, d(u), d(skip) written once
                 nbytes = 6.0 * args[13] * args[14] * args[15] * 32 * 2
             self.pending.append((kname, flops, start, ev, name, self._shape(name, args), nbytes))
-            if name in ("sd_conv_gemm", "sd_conv_gemm_bnfin") and self._last_phase == "fwd":
+            if name == "sd_conv_gemm" and self._last_phase == "fwd":
                 # forward order (model.py:79-104): the first 10 3x3 convs are enc1..enc4, bottleneck
                 if self._fwd_conv < 10 and args[1].taps == 9:
                     self.encoder.append((self._fwd_conv, flops, self._min_bytes(args), start, ev))
@@ -192,7 +189,7 @@ class GemmTimer:
             return f"bwd_fused P={args[14] * args[15] * args[16]} C=32"
         if name == "sd_conv3x3_bwd_fused_dec":
             return f"bwd_fused_dec P={args[13] * args[14] * args[15]} C=64->32"
-        if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum", "sd_conv_gemm_bnfin"):
+        if name in ("sd_conv_gemm", "sd_conv_gemm_bnsum"):
             s = args[1]
             return f"fwd M={args[2] * args[3] * args[4]} N={args[6]} K={s.taps}x{s.chans[0] + s.chans[1]}"
         b = args[2]

@@ -117,14 +117,6 @@ int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, void* out, sd
  *                    (sd_stat_rows_sum) */
 int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi,
                  void* out0, void* out1, int n_split, const float* bias, float* stats, sd_stream s);
-/* sd_conv_gemm(SD_EPI_STATS) whose last block also runs sd_bn_fwd_finalize (same operands; count = batch*H*W),
- * so no finalize launch follows the conv: bf16 3x3 halo shapes, N = 32 * 2^k. counter: one int, zero before the
- * first launch (the last block resets it), not shared by launches that may run concurrently. */
-int sd_conv_gemm_bnfin_ok(int dtype, const sd_src* a, int N);
-int sd_conv_gemm_bnfin(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N, int kpad,
-                       void* out, float* stats, int* counter, const float* gamma, const float* beta,
-                       float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* mean,
-                       float* invstd, float* scale, float* shift, sd_stream s);
 /* number of float2 stat rows sd_conv_gemm(SD_EPI_STATS) writes for this shape */
 int sd_conv_gemm_stat_rows(int dtype, int batch, int H, int W, int N);
 /* name of the kernel instance sd_conv_gemm / sd_wgrad_gemm launches for a shape (as rocprofv3 shows it) */

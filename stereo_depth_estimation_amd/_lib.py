@@ -125,9 +125,6 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_conv_gemm": (_i, [_i, _SRC, _i, _i, _i, _p, _i, _i, _i, _p, _p, _i, _p, _p, _p]),
     "sd_conv_gemm_stat_rows": (_i, [_i, _i, _i, _i, _i]),
     "sd_conv_gemm_bnsum": (_i, [_i, _SRC, _i, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
-    "sd_conv_gemm_bnfin_ok": (_i, [_i, _SRC, _i]),
-    "sd_conv_gemm_bnfin": (_i, [_i, _SRC, _i, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p,
-                                _p, _p]),
     "sd_conv_gemm_bnsum_ok": (_i, [_i, _SRC, _i]),
     "sd_conv_gemm_bnsum_rows": (_i, [_SRC, _i, _i, _i, _i]),
     "sd_conv_gemm_bnsum_kernel_name": (ctypes.c_char_p, [_SRC, _i, _i, _i]),

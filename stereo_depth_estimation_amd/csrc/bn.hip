@@ -42,7 +42,28 @@ __device__ __forceinline__ void block_sum2(double& a, double& b) {
     b = red[1][0];
 }
 
-// bn_fwd_emit: common.h (shared with the finalize in the conv's last block, conv_halo.hip)
+// mean/invstd/scale/shift and the running-statistics update of channel c from its fp64 (sum, sumsq) over `count`
+// pixels (every rank's, with SyncBatchNorm: the unbiased variance then uses the global count, as torch's)
+__device__ __forceinline__ void bn_fwd_emit(int c, double s, double ss, double count, const float* gamma,
+                                            const float* beta, float* running_mean, float* running_var, int64_t* nbt,
+                                            float momentum, float eps, float* mean_o, float* invstd_o, float* scale_o,
+                                            float* shift_o) {
+    const double mean = s / count;
+    double var = ss / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * invstd;
+    mean_o[c] = (float)mean;
+    invstd_o[c] = invstd;
+    scale_o[c] = sc;
+    shift_o[c] = beta[c] - (float)mean * sc;
+    if (running_mean) {
+        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        running_mean[c] = (float)(momentum * mean + (1.0 - momentum) * (double)running_mean[c]);
+        running_var[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)running_var[c]);
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+}
 
 __global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restrict__ stats, int rows, int C,
                                                          double count, const float* gamma, const float* beta,

@@ -33,41 +33,6 @@ struct HaloBnSum {
     const float *scale, *shift, *mean, *invstd;
 };
 
-// The BatchNorm forward finalize run by the last block of a STATS conv launch (sd_conv_gemm_bnfin -> conv_halo.hip):
-// the sd_bn_fwd_finalize operands plus a zeroed launch counter (the last block resets it)
-struct HaloBnFin {
-    int* counter;
-    const float *gamma, *beta;
-    float *running_mean, *running_var;
-    int64_t* nbt;
-    float momentum, eps;
-    double count;
-    float *mean, *invstd, *scale, *shift;
-};
-
-// mean/invstd/scale/shift and the running-statistics update of channel c from its fp64 (sum, sumsq) over `count`
-// pixels (every rank's, with SyncBatchNorm: the unbiased variance then uses the global count, as torch's)
-__device__ __forceinline__ void bn_fwd_emit(int c, double s, double ss, double count, const float* gamma,
-                                            const float* beta, float* running_mean, float* running_var, int64_t* nbt,
-                                            float momentum, float eps, float* mean_o, float* invstd_o, float* scale_o,
-                                            float* shift_o) {
-    const double mean = s / count;
-    double var = ss / count - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * invstd;
-    mean_o[c] = (float)mean;
-    invstd_o[c] = invstd;
-    scale_o[c] = sc;
-    shift_o[c] = beta[c] - (float)mean * sc;
-    if (running_mean) {
-        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-        running_mean[c] = (float)(momentum * mean + (1.0 - momentum) * (double)running_mean[c]);
-        running_var[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)running_var[c]);
-    }
-    if (nbt && c == 0) nbt[0] += 1;
-}
-
 // BatchNorm-backward operands of the fused weight gradient (sd_wgrad_gemm_bnbwd -> conv_halo.hip)
 struct HaloBnBwd {
     const void* da;

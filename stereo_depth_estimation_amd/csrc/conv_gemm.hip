@@ -280,7 +280,7 @@ const char* sd_halo_fwd_name(int H, int W, int N, int epi, int c0, int c1, bool 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns = nullptr,
                      bool wsplit = false, const float* osc = nullptr, const float* osh = nullptr, void* ws = nullptr,
-                     long long ws_bytes = 0, const HaloBnFin* fin = nullptr);
+                     long long ws_bytes = 0);
 long long sd_halo_split_ws_bytes(const sd_src& a, int batch, int H, int W, int N, int epi, bool wsplit);
 int sd_halo_store_rows(int batch, int H, int W, int N, int ctot);
 bool sd_halo_bnsum_ok(const sd_src& a, int N);
@@ -410,29 +410,6 @@ extern "C" int sd_conv_gemm_bnsum(int dtype, const sd_src* a, int batch, int H, 
     SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == H && g.Wl == W, "sd_conv_gemm_bnsum: kpad/grid");
     return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, SD_EPI_STORE, out, nullptr, 0, partials, to_stream(s),
                             &bns);
-}
-
-extern "C" int sd_conv_gemm_bnfin_ok(int dtype, const sd_src* a, int N) {
-    if (dtype != SD_BF16 || !a || !sd_halo_fwd_ok(*a, N, SD_EPI_STATS)) return 0;
-    return (N <= 256 ? 256 % N == 0 : N % 256 == 0) ? 1 : 0;
-}
-
-extern "C" int sd_conv_gemm_bnfin(int dtype, const sd_src* a, int batch, int H, int W, const void* wpack, int N,
-                                  int kpad, void* out, float* stats, int* counter, const float* gamma,
-                                  const float* beta, float* running_mean, float* running_var, int64_t* nbt,
-                                  float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
-                                  sd_stream s) {
-    if (int e = validate_src(a, "sd_conv_gemm_bnfin")) return e;
-    SD_REQUIRE(sd_conv_gemm_bnfin_ok(dtype, a, N), "sd_conv_gemm_bnfin: bf16 3x3 halo STATS shapes only (_ok)");
-    SD_REQUIRE(batch > 0 && H > 0 && W > 0 && wpack && out && stats && counter && gamma && beta && mean && invstd &&
-                   scale && shift && (running_mean == nullptr) == (running_var == nullptr),
-               "sd_conv_gemm_bnfin: bad args");
-    GatherSrc g = make_gather(*a);
-    SD_REQUIRE(kpad % 64 == 0 && kpad >= g.kchunks * 8 && g.Hl == H && g.Wl == W, "sd_conv_gemm_bnfin: kpad/grid");
-    const HaloBnFin fin{counter, gamma, beta, running_mean, running_var, nbt, momentum, eps,
-                        (double)batch * H * W, mean, invstd, scale, shift};
-    return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, SD_EPI_STATS, out, nullptr, 0, stats, to_stream(s),
-                            nullptr, false, nullptr, nullptr, nullptr, 0, &fin);
 }
 
 extern "C" int sd_conv3x3_ex_ok(const sd_src* a, int N) {

@@ -212,56 +212,7 @@ struct HFwdArgs {
     int ksplit, gblk, cps;
     int npix;  // batch * H * W (partials rows per group)
     float* part;
-    HaloBnFin fin;  // fin.counter != null: the launch's last block runs the BatchNorm finalize (sd_conv_gemm_bnfin)
 };
-
-// The BatchNorm forward finalize by the last block of a STATS launch (MI355X_MICROARCH.md, inter-workgroup hand-off:
-// every block stores its statistics row with sc1 stores, waits for them, and one lane adds to an agent-scope counter;
-// the block whose add returns nblocks - 1 reads all rows with sc1 loads after a workgroup barrier). Fixed summation
-// order: channel c's rows g, g + G, ... per thread group g in fp64, then the G partials in order. Called by the 256
-// MFMA-wave threads (the loader waves have exited); red: 4 KB of free LDS.
-__device__ void halo_bn_fin(const HFwdArgs& p, int tid, double* red) {
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics stores have completed
-    __syncthreads();
-    if (tid == 0) {
-        const int nb = gridDim.x * gridDim.y * gridDim.z;
-        s_last = __hip_atomic_fetch_add(p.fin.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    const int N = p.N, rows = p.gper;
-    const unsigned long long* st = reinterpret_cast<const unsigned long long*>(p.stats);
-    const int G = N <= 256 ? 256 / N : 1, CPT = N <= 256 ? 1 : N / 256;  // row groups; channels per thread
-    const int g = tid / (256 / G) , cl = tid % (256 / G);
-    for (int k = 0; k < CPT; ++k) {
-        const int c = cl + k * 256;
-        double sm = 0.0, sq = 0.0;
-        if (c < N) {
-#pragma unroll 8
-            for (int r = g; r < rows; r += G) {
-                const unsigned long long v =
-                    __hip_atomic_load(st + (size_t)r * N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                sm += (double)__uint_as_float((unsigned)v);
-                sq += (double)__uint_as_float((unsigned)(v >> 32));
-            }
-        }
-        red[tid] = sm;
-        red[256 + tid] = sq;
-        __syncthreads();
-        if (g == 0 && c < N) {
-            double a = red[cl], b = red[256 + cl];
-            for (int h = 1; h < G; ++h) {
-                a += red[h * (256 / G) + cl];
-                b += red[256 + h * (256 / G) + cl];
-            }
-            bn_fwd_emit(c, a, b, p.fin.count, p.fin.gamma, p.fin.beta, p.fin.running_mean, p.fin.running_var,
-                        p.fin.nbt, p.fin.momentum, p.fin.eps, p.fin.mean, p.fin.invstd, p.fin.scale, p.fin.shift);
-        }
-        __syncthreads();
-    }
-    if (tid == 0) __hip_atomic_store(p.fin.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-}
 
 // Cache policy of the conv epilogue stores: nontemporal (2). The outputs (0.1-0.3 GB per launch) are read by the next
 // layer's kernel, never again by this one, and allocating them in the XCD's 4 MB L2 evicts the weight rows and halo
@@ -1455,16 +1406,7 @@ __device__ __forceinline__ void halo_conv_body(const HFwdArgs& p) {
             s += redf[(w * BN + tid) * 2];
             ss += redf[(w * BN + tid) * 2 + 1];
         }
-        float2* dst = reinterpret_cast<float2*>(p.stats) + (size_t)slot * p.N + n0 + tid;
-        if (STATS && p.fin.counter)  // sc1: read by the last block, maybe on another XCD
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst),
-                               (unsigned long long)__float_as_uint(s) | ((unsigned long long)__float_as_uint(ss) << 32),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            *dst = make_float2(s, ss);
-    }
-    if constexpr (STATS) {
-        if (p.fin.counter) halo_bn_fin(p, tid, reinterpret_cast<double*>(smem));
+        reinterpret_cast<float2*>(p.stats)[(size_t)slot * p.N + n0 + tid] = make_float2(s, ss);
     }
 }
 
@@ -2497,7 +2439,7 @@ long long sd_halo_split_ws_bytes(const sd_src& a, int batch, int H, int W, int N
 
 int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                      void* out1, int n_split, float* stats, hipStream_t st, const HaloBnSum* bns, bool wsplit,
-                     const float* osc, const float* osh, void* ws, long long ws_bytes, const HaloBnFin* fin) {
+                     const float* osc, const float* osh, void* ws, long long ws_bytes) {
     const bool st_ = epi == SD_EPI_STATS || epi == SD_EPI_SPLIT_STATS;
     const HTile t = fwd_tile(a.chans[0] + a.chans[1], H, W, N, st_);
     HFwdArgs p;
@@ -2554,12 +2496,6 @@ int sd_halo_conv_fwd(const sd_src& a, int batch, int H, int W, const void* wpack
     p.xcd = halo_xcd_enabled() && (p.gblk * q.ksplit) % 8 == 0;
     p.prio = halo_prio(a);
     p.dbg = g_wg_dbg;
-    p.fin = HaloBnFin{};
-    if (fin) {
-        SD_REQUIRE(epi == SD_EPI_STATS && q.ksplit == 1 && fin->counter && (N <= 256 ? 256 % N == 0 : N % 256 == 0),
-                   "sd_conv_gemm_bnfin: a STATS launch with N = 32 * 2^k (got N=%d)", N);
-        p.fin = *fin;
-    }
     const int cap = t.it == 2 ? 384 : halo_px_cap(t.rt, t.ck);
     SD_REQUIRE(t.rt >= 2 && t.rt <= 4 && p.nhalo <= cap && t.th * t.tw <= 128 * t.rt &&
                    t.th < 64 && t.tw < 512,

@@ -231,8 +231,6 @@ class UNetEngine:
         # (sd_conv3x3_bwd_fused / _dec: dy stays in LDS; SD_BWD_FUSE=0: weight gradient + dgrad launches;
         # SD_BWD_FUSE=1: the conv1 layers only)
         self.bwd_fuse = {"0": 0, "1": 1}.get(os.environ.get("SD_BWD_FUSE", "2"), 2)
-        # the forward BatchNorm finalize in the conv's last block (sd_conv_gemm_bnfin; SD_BN_FIN=0: its own launch)
-        self.bn_fin = os.environ.get("SD_BN_FIN", "1") != "0"
         self._bnsum_rows: dict[str, int] = {}
         # training: the split-K slab reduce of every weight gradient on a second stream (SD_SIDE_REDUCE=1), so it
         # overlaps the next layer's kernels instead of adding a kernel boundary to the critical path; 2: the
@@ -388,8 +386,6 @@ class UNetEngine:
                 # or the fused dec1.0 backward's d(up) column-sum rows (sd_conv3x3_bwd_fused_dec)
                 max_stat = max(max_stat, L.call("sd_conv3x3_bwd_fused_splits", B, H, W) * 32 * 2)
         t["stats"] = torch.empty(max_stat, dtype=f32, device=dev)
-        # the launch counter of sd_conv_gemm_bnfin (zero between launches: each launch's last block resets it)
-        t["fin_ctr"] = torch.zeros(4, dtype=torch.int32, device=dev)
         for u in self.ups.values():
             t["u:" + u.name] = act(u.level - 1, u.cout)
         if self.sd_dtype == L.SD_BF16:
@@ -543,14 +539,6 @@ class UNetEngine:
             if split:
                 L.call("sd_conv3x3_ex", src, ws.B, Hl, Wl, self._ws_ptr(cl.off_s), cl.cout, cl.kpad_s,
                        L.SD_EPI_STATS, L.SD_CONV_WSPLIT, None, None, y.data_ptr(), stats.data_ptr(), s)
-            elif self.bn_fin and self.bn_sync is None and L.call("sd_conv_gemm_bnfin_ok", dt, src, cl.cout) == 1:
-                # the conv's last block runs the BatchNorm finalize: no finalize launch between two convs
-                rm, rv = self.bufs[cl.bn_key + ".running_mean"], self.bufs[cl.bn_key + ".running_var"]
-                L.call("sd_conv_gemm_bnfin", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f,
-                       y.data_ptr(), stats.data_ptr(), t["fin_ctr"].data_ptr(), g.data_ptr(), b.data_ptr(),
-                       rm.data_ptr(), rv.data_ptr(), L.ptr(self.bufs.get(cl.bn_key + ".num_batches_tracked")),
-                       BN_MOMENTUM, BN_EPS, mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
-                return
             else:
                 L.call("sd_conv_gemm", dt, src, ws.B, Hl, Wl, self._wp(cl.off_f), cl.cout, cl.kpad_f, L.SD_EPI_STATS,
                        y.data_ptr(), None, 0, None, stats.data_ptr(), s)

@@ -1018,48 +1018,3 @@ def test_conv3x3_bwd_fused_dec_matches_reference(B, H, W):
     assert float(((got - dx_ref).abs() - 2.0 ** -7 * dx_ref.abs()).max()) <= 1e-3 * float(dx_ref.abs().max())
     b_ref = got[:, :C].sum((0, 2, 3))
     assert float((bias.double().cpu() - b_ref).abs().max()) <= 1e-4 * (1 + float(b_ref.abs().max()))
-
-
-@pytest.mark.parametrize("B,H,W,ci,co", [(2, 24, 64, 32, 32), (2, 16, 32, 32, 64), (1, 12, 20, 64, 128),
-                                         (2, 6, 10, 128, 256), (2, 4, 5, 256, 512)])
-def test_conv_gemm_bnfin_matches_stats_plus_finalize(B, H, W, ci, co):
-    """sd_conv_gemm_bnfin (the BatchNorm forward finalize run by the conv launch's last block, after an agent-scope
-    counter hand-off) against sd_conv_gemm(STATS) + sd_bn_fwd_finalize on the same operands: the stored y bit-identical,
-    mean / invstd / scale / shift / running statistics within fp32 rounding (both sum the same rows in fp64, in another
-    order), num_batches_tracked +1 per launch; three launches in a row (the counter must come back to zero)."""
-    lib = L()
-    torch.manual_seed(5)
-    y0 = torch.randn(B * H * W, ci, device=DEV).to(torch.bfloat16)
-    sc0, sh0 = torch.rand(ci, device=DEV) + 0.5, torch.randn(ci, device=DEV) * 0.2
-    src = lib.make_src(y0, ci, H, W, taps=9, bn0=(sc0, sh0))
-    assert lib.call("sd_conv_gemm_bnfin_ok", lib.SD_BF16, src, co) == 1
-    w = torch.randn(co, ci, 3, 3) / (3.0 * ci ** 0.5)
-    wp, kpad = _pack3(w, ci, False, "bf16")
-    rows = lib.call("sd_conv_gemm_stat_rows", lib.SD_BF16, B, H, W, co)
-    g, b = torch.rand(co, device=DEV) + 0.5, torch.randn(co, device=DEV) * 0.1
-    outs = {}
-    for mode in ("ref", "fin"):
-        rm, rv = torch.zeros(co, device=DEV), torch.ones(co, device=DEV)
-        nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
-        y = torch.empty(B * H * W, co, device=DEV, dtype=torch.bfloat16)
-        stats = torch.full((rows * co * 2,), float("nan"), device=DEV)
-        ctr = torch.zeros(4, dtype=torch.int32, device=DEV)
-        res = [torch.empty(co, device=DEV) for _ in range(4)]
-        for _ in range(3):
-            if mode == "ref":
-                lib.call("sd_conv_gemm", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, lib.SD_EPI_STATS,
-                         y.data_ptr(), None, 0, None, stats.data_ptr(), lib.stream_handle())
-                lib.call("sd_bn_fwd_finalize", stats.data_ptr(), rows, co, float(B * H * W), g.data_ptr(),
-                         b.data_ptr(), rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(), 0.1, 1e-5,
-                         *[t.data_ptr() for t in res], lib.stream_handle())
-            else:
-                lib.call("sd_conv_gemm_bnfin", lib.SD_BF16, src, B, H, W, wp.data_ptr(), co, kpad, y.data_ptr(),
-                         stats.data_ptr(), ctr.data_ptr(), g.data_ptr(), b.data_ptr(), rm.data_ptr(), rv.data_ptr(),
-                         nbt.data_ptr(), 0.1, 1e-5, *[t.data_ptr() for t in res], lib.stream_handle())
-        torch.cuda.synchronize()
-        outs[mode] = (y.clone(), [t.clone() for t in res], rm.clone(), rv.clone(), int(nbt.item()), ctr.clone())
-    (y0_, r0, rm0, rv0, n0, _), (y1_, r1, rm1, rv1, n1, c1) = outs["ref"], outs["fin"]
-    assert torch.equal(y0_, y1_)
-    for a, e in zip(r1 + [rm1, rv1], r0 + [rm0, rv0]):
-        assert torch.allclose(a, e, rtol=2e-6, atol=1e-6), float((a - e).abs().max())
-    assert n0 == n1 == 3 and int(c1.abs().sum()) == 0
