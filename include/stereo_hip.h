@@ -38,7 +38,7 @@ enum { SD_IDENT = 0, SD_BNRELU = 1, SD_AFFINE = 2 };
 /* conv-GEMM epilogues */
 enum { SD_EPI_STORE = 0, SD_EPI_STATS = 1, SD_EPI_SPLIT = 2, SD_EPI_PIXSHUF = 3, SD_EPI_SPLIT_STATS = 4 };
 /* weight-gradient layouts */
-enum { SD_W_CONV3 = 0, SD_W_CONVT = 1 };
+enum { SD_W_CONV3 = 0, SD_W_CONVT = 1, SD_W_ROWSUM = 2 };
 /* heads modes */
 enum { SD_HEADS_INFER = 0, SD_HEADS_LOSS = 1, SD_HEADS_GRADS = 2 };
 
@@ -186,7 +186,10 @@ const char* sd_wgrad_bnbwd_kernel_name(const sd_src* a, const sd_src* b, int M, 
  *   SD_W_CONVT: M = ci, N = 4*co     -> dw[ci][co][2][2] */
 int sd_wgrad_reduce(const float* slab, int splits, int M, int N, int layout, int ci_real, float* dw, sd_stream s);
 /* up to 48 of those reduces in ONE launch, each bit-identical to its sd_wgrad_reduce call (the slabs must be
- * distinct buffers: the engine defers a step's reduces into one launch per gradient-ready group) */
+ * distinct buffers: the engine defers a step's reduces into one launch per gradient-ready group).
+ * layout SD_W_ROWSUM: dw[c] = sum over r < splits of ((const float2*)slab)[r * N + c].x for c < ci_real (M = 1),
+ * bit-identical to sd_stat_rows_sum(slab, splits, N, ci_real, dw): the ConvTranspose2d bias gradients joined to the
+ * batch instead of a launch each */
 typedef struct sd_wred_job {
     const float* slab;
     int splits, M, N, layout, ci_real;
@@ -357,7 +360,8 @@ int sd_conv3x3_bwd_fused_dec(const void* da, const void* y, const float* scale, 
 
 /* ---- AdamW (train.py:343,578; torch 2.10 single-tensor AdamW, decoupled weight decay) ----
  * One flat fp32 parameter/gradient/state buffer (all tensors share lr/betas/eps/wd).
- * The step is skipped (and *step not advanced) when *count == 0 (train.py:331-332). */
+ * The step is skipped (and *step not advanced) when *count == 0 (train.py:331-332). One launch: scratch[0] is the
+ * kernel's block counter (zero before the first call; every call leaves it zero). */
 int sd_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double weight_decay, double beta1,
              double beta2, double eps, int* step, const int* count, float* scratch /* 4 floats */, sd_stream s);
 

@@ -20,7 +20,7 @@ LIB_PATH = Path(os.environ.get("SD_HIP_LIB") or Path(__file__).resolve().parent 
 SD_F32, SD_BF16 = 0, 1
 SD_IDENT, SD_BNRELU, SD_AFFINE = 0, 1, 2
 SD_EPI_STORE, SD_EPI_STATS, SD_EPI_SPLIT, SD_EPI_PIXSHUF, SD_EPI_SPLIT_STATS = 0, 1, 2, 3, 4
-SD_W_CONV3, SD_W_CONVT = 0, 1
+SD_W_CONV3, SD_W_CONVT, SD_W_ROWSUM = 0, 1, 2
 SD_HEADS_INFER, SD_HEADS_LOSS, SD_HEADS_GRADS = 0, 1, 2
 
 _p = ctypes.c_void_p

@@ -8,40 +8,7 @@
 
 namespace {
 
-// ------------------------------------------------------------------ finalize (one block per channel)
-template <int NT>
-__device__ __forceinline__ void block_sum2(double& a, double& b) {
-    static_assert(NT >= 64 && (NT & (NT - 1)) == 0, "whole waves, a power of two");
-    // the tree t += t + s for s = NT/2 .. 1: the steps across waves through LDS, the last six (s < 64) as shuffles in
-    // wave 0 with the same pairs and order (bit-identical sums; 8 -> 3 barriers: these launches are latency-bound)
-    __shared__ double red[2][NT];
-    red[0][threadIdx.x] = a;
-    red[1][threadIdx.x] = b;
-    __syncthreads();
-    for (int s = NT / 2; s >= 64; s >>= 1) {
-        if (threadIdx.x < s) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + s];
-            red[1][threadIdx.x] += red[1][threadIdx.x + s];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x < 64) {
-        double x = red[0][threadIdx.x], y = red[1][threadIdx.x];
-#pragma unroll
-        for (int s = 32; s > 0; s >>= 1) {
-            x += __shfl_down(x, s);
-            y += __shfl_down(y, s);
-        }
-        if (threadIdx.x == 0) {
-            red[0][0] = x;
-            red[1][0] = y;
-        }
-    }
-    __syncthreads();
-    a = red[0][0];
-    b = red[1][0];
-}
-
+// ------------------------------------------------------------------ finalize (one block per channel; block_sum2 in common.h)
 // mean/invstd/scale/shift and the running-statistics update of channel c from its fp64 (sum, sumsq) over `count`
 // pixels (every rank's, with SyncBatchNorm: the unbiased variance then uses the global count, as torch's)
 __device__ __forceinline__ void bn_fwd_emit(int c, double s, double ss, double count, const float* gamma,

@@ -273,32 +273,32 @@ __global__ __launch_bounds__(256) void k_pack_multi(const PackJobs P, T* __restr
 
 // ------------------------------------------------------------------ AdamW
 struct AdamScalars {
-    int skip;
     float decay;      // 1 - lr*wd
     float step_size;  // lr / (1 - b1^t)
     float bc2_sqrt;   // sqrt(1 - b2^t)
 };
 
-__global__ void k_adamw_prep(int* step, const int* count, double lr, double wd, double b1, double b2,
-                             AdamScalars* sc) {
-    const int skip = (count != nullptr && *count == 0) ? 1 : 0;
-    sc->skip = skip;
-    if (skip) return;
-    const int t = *step + 1;
-    *step = t;
+// the step's scalars from step t in fp64 (outside the contract(off) region below: the same code the former one-thread
+// prep launch ran, so the updates are unchanged)
+__device__ __forceinline__ AdamScalars adam_scalars(int t, double lr, double wd, double b1, double b2) {
     const double bc1 = 1.0 - pow(b1, (double)t);
     const double bc2 = 1.0 - pow(b2, (double)t);
-    sc->decay = (float)(1.0 - lr * wd);
-    sc->step_size = (float)(lr / bc1);
-    sc->bc2_sqrt = (float)sqrt(bc2);
+    return AdamScalars{(float)(1.0 - lr * wd), (float)(lr / bc1), (float)sqrt(bc2)};
 }
 
+// One launch per step: every wave derives the scalars from *step itself, and the step counter advances once every
+// block has read it: each block counts itself out on `done` (an agent-scope relaxed add after a barrier, so all of
+// its waves have read *step), and the block that counts last writes step + 1 and re-arms the counter. Skipped
+// steps (*count == 0, train.py:331-332) touch neither.
 #pragma clang fp contract(off)
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v, long long n, float w1,
-                                               float b2, float w2, float eps, const AdamScalars* sc) {
-    if (sc->skip) return;
-    const float decay = sc->decay, step_size = sc->step_size, bc2s = sc->bc2_sqrt;
+                                               float b2, float w2, float eps, int* step, const int* count, double lr,
+                                               double wd, double b1d, double b2d, unsigned* done) {
+    if (count != nullptr && *count == 0) return;
+    const int t = *step + 1;
+    const AdamScalars sc = adam_scalars(t, lr, wd, b1d, b2d);
+    const float decay = sc.decay, step_size = sc.step_size, bc2s = sc.bc2_sqrt;
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const float gi = g[i];
         float pi = p[i] * decay;                  // param.mul_(1 - lr*wd)
@@ -311,6 +311,14 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
         p[i] = pi;
         m[i] = mi;
         v[i] = vi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            *step = t;
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 #pragma clang fp contract(on)
@@ -464,14 +472,10 @@ extern "C" int sd_adamw(float* p, const float* g, float* m, float* v, int64_t n,
                           double beta1, double beta2, double eps, int* step, const int* count, float* scratch,
                           sd_stream s) {
     SD_REQUIRE(p && g && m && v && n > 0 && step && scratch, "sd_adamw: bad args");
-    AdamScalars* sc = reinterpret_cast<AdamScalars*>(scratch);
-    hipLaunchKernelGGL(k_adamw_prep, dim3(1), dim3(1), 0, to_stream(s), step, count, lr, weight_decay, beta1, beta2,
-                       sc);
-    if (int e = sd_check_launch("sd_adamw(prep)")) return e;
     const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2);
     const int grid = grid_for(n);
     hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, to_stream(s), p, g, m, v, (long long)n, w1, (float)beta2,
-                       w2, (float)eps, sc);
+                       w2, (float)eps, step, count, lr, weight_decay, beta1, beta2, reinterpret_cast<unsigned*>(scratch));
     return sd_check_launch("sd_adamw");
 }
 

@@ -277,6 +277,8 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
 // Many weight gradients' slab reduces in ONE launch (sd_wgrad_reduce_batch): job j owns blocks [b0, b0 + nblk) and
 // runs exactly the single-job reduce of sd_wgrad_reduce (same G, same block count, so the same summation order and
 // bit-identical gradients). A step's 22 reduces were 22 kernel boundaries with small, low-occupancy tails each.
+// SD_W_ROWSUM jobs are the ConvTranspose2d bias gradients: column sums of the statistics rows the decoder dgrad
+// epilogue left (what sd_stat_rows_sum computes in a launch of its own), one block per channel.
 constexpr int WRED_MAX = 48;
 struct WRedJob {
     const float* slab;
@@ -295,6 +297,15 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_batch(const WRedBatch b) {
     for (int i = 1; i < b.n; ++i) k = (int)blockIdx.x >= b.j[i].b0 ? i : k;  // block-uniform (scalar) job lookup
     const WRedJob& j = b.j[k];
     const int bid = blockIdx.x - j.b0;
+    if (j.layout == SD_W_ROWSUM) {
+        // column bid of `splits` float2 rows of pitch N, .x summed in fp64: k_sum_finalize's order, bit-identical
+        const float2* rows = reinterpret_cast<const float2*>(j.slab);
+        double s = 0.0, ss = 0.0;
+        for (int r = threadIdx.x; r < j.splits; r += 256) s += rows[(size_t)r * j.N + bid].x;
+        block_sum2<256>(s, ss);
+        if (threadIdx.x == 0) j.dw[bid] = (float)s;
+        return;
+    }
     if (j.g == 32)
         wgrad_reduce_body<32>(j.slab, j.splits, j.total4, j.N, j.layout, j.ci_pad, j.ci_real, j.dw, bid, j.nblk, part);
     else if (j.g == 8)
@@ -471,9 +482,16 @@ extern "C" int sd_wgrad_reduce_batch(const sd_wred_job* jobs, int njobs, sd_stre
     for (int i = 0; i < njobs; ++i) {
         const sd_wred_job& q = jobs[i];
         int ci_pad = 0, blocks = 0, g = 8;
-        if (int e = wred_plan(q.slab, q.splits, q.M, q.N, q.layout, q.ci_real, q.dw, "sd_wgrad_reduce_batch", ci_pad,
-                              g, blocks))
+        if (q.layout == SD_W_ROWSUM) {  // rows = splits, pitch N float2, channels ci_real
+            SD_REQUIRE(q.slab && q.dw && q.splits > 0 && q.M == 1 && q.ci_real > 0 && q.ci_real <= q.N &&
+                           ((uintptr_t)q.slab & 7) == 0,
+                       "sd_wgrad_reduce_batch: row-sum job %d: rows %d, M %d, N %d, C %d", i, q.splits, q.M, q.N,
+                       q.ci_real);
+            blocks = q.ci_real;
+        } else if (int e = wred_plan(q.slab, q.splits, q.M, q.N, q.layout, q.ci_real, q.dw, "sd_wgrad_reduce_batch",
+                                     ci_pad, g, blocks)) {
             return e;
+        }
         b.j[i] = WRedJob{q.slab, q.dw, (long long)q.M * q.N / 4, q.splits, q.N, q.layout, ci_pad, q.ci_real, g,
                          (int)total_blocks, blocks};
         total_blocks += blocks;

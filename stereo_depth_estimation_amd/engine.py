@@ -25,6 +25,7 @@ BN_MOMENTUM = 0.1
 BLOCKS_FWD = ("enc1", "enc2", "enc3", "enc4", "bottleneck", "dec4", "dec3", "dec2", "dec1")
 LEVEL = {"enc1": 0, "enc2": 1, "enc3": 2, "enc4": 3, "bottleneck": 4, "dec4": 3, "dec3": 2, "dec2": 1, "dec1": 0}
 UP_OF_DEC = {"dec4": "up4", "dec3": "up3", "dec2": "up2", "dec1": "up1"}
+DEC_OF_UP = {u: d for d, u in UP_OF_DEC.items()}
 SKIP_OF_DEC = {"dec4": "enc4", "dec3": "enc3", "dec2": "enc2", "dec1": "enc1"}
 UP_SRC = {"up4": "bottleneck", "up3": "dec4", "up2": "dec3", "up1": "dec2"}
 PREV_ENC = {"enc2": "enc1", "enc3": "enc2", "enc4": "enc3", "bottleneck": "enc4"}
@@ -461,6 +462,14 @@ class UNetEngine:
                     sp = L.call("sd_wgrad_splits", dt, B, H >> lv, W >> lv, u.cin, 4 * u.cout)
                     ws.slab_off[u.name] = tot
                     tot += _r16(sp * u.cin * 4 * u.cout)
+                    # the statistics rows of d(up) the decoder dgrad leaves for this layer's bias gradient, summed in
+                    # the deferred batch (an SD_W_ROWSUM job) instead of a launch of their own
+                    dec0 = self.convs[DEC_OF_UP[u.name] + ".0"]
+                    Hd, Wd = H >> dec0.level, W >> dec0.level
+                    rows = L.call("sd_conv_gemm_stat_rows", dt, B, Hd, Wd, dec0.cin) * dec0.cin * 2
+                    rows = max(rows, L.call("sd_conv3x3_bwd_fused_splits", B, Hd, Wd) * 32 * 2)
+                    ws.slab_off["brows:" + u.name] = tot
+                    tot += _r16(rows)
                 max_slab = tot
             t["slab"] = torch.empty(max_slab, dtype=f32, device=dev)
             if self.side_mode:
@@ -1043,6 +1052,13 @@ class UNetEngine:
         ev.record(side)
         self._slab_free[i] = ev
 
+    def _bias_rows_ptr(self, up_name: str) -> int:
+        """Where the decoder dgrad writes the d(up) statistics rows of up_name's bias gradient: its own region of the
+        slab buffer when the reduces are deferred (they are summed at the flush), else the shared t["stats"]."""
+        if self.defer_reduce:
+            return self.ws.t["slab"].data_ptr() + 4 * self.ws.slab_off["brows:" + up_name]
+        return self.ws.t["stats"].data_ptr()
+
     def _flush_reduces(self):
         """Every deferred slab reduce in one launch (the gradients they write are final after it, in stream order)."""
         if self._red_jobs:
@@ -1072,11 +1088,11 @@ class UNetEngine:
                     t["invstd:" + cl.name].data_ptr(), t["coef:" + cl.name].data_ptr(), t["u:" + up.name].data_ptr(),
                     t["y:" + sk.name].data_ptr(), ssc.data_ptr(), ssh.data_ptr(), self._wp(cl.off_d), cl.kpad_d,
                     ws.B, Hl, Wl, t["du:" + up.name].data_ptr(), t["dskip:" + up.name].data_ptr())
-            self._wgrad_slabs(lambda slab, st: L.call("sd_conv3x3_bwd_fused_dec", *args, slab,
-                                                      t["stats"].data_ptr(), st),
+            brows = self._bias_rows_ptr(up.name)
+            self._wgrad_slabs(lambda slab, st: L.call("sd_conv3x3_bwd_fused_dec", *args, slab, brows, st),
                               sp, cl.cout, 9 * cl.cin_pad, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key],
                               gemm_may_side=False, key=cl.name)
-            self._up_bias_rows = (sp, 32)
+            self._up_bias_rows = (sp, 32, brows)
             return
         if kind == 1:
             # one pass: dy = BatchNorm-backward(da, y) staged in LDS, the weight gradient's split-K slabs, the dgrad
@@ -1146,10 +1162,12 @@ class UNetEngine:
                 up = self.ups[UP_OF_DEC[cl.blk]]
                 # bf16: the same epilogue sums d(up) per channel = the ConvTranspose2d bias gradient (_up_bwd)
                 sums = self.bias_fuse and dt == L.SD_BF16 and (cl.cin == 32 or cl.cin % 64 == 0)
+                brows = self._bias_rows_ptr(up.name) if sums else None
                 L.call("sd_conv_gemm", dt, dsrc, ws.B, Hl, Wl, self._wp(cl.off_d), cl.cin, cl.kpad_d,
                        L.SD_EPI_SPLIT_STATS if sums else L.SD_EPI_SPLIT, t["du:" + up.name].data_ptr(),
-                       t["dskip:" + up.name].data_ptr(), up.cout, None, t["stats"].data_ptr() if sums else None, s)
-                self._up_bias_rows = (L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cin), cl.cin) if sums else None
+                       t["dskip:" + up.name].data_ptr(), up.cout, None, brows, s)
+                self._up_bias_rows = ((L.call("sd_conv_gemm_stat_rows", dt, ws.B, Hl, Wl, cl.cin), cl.cin, brows)
+                                      if sums else None)
         if not fuse:
             self._wgrad(a, b, cl.level, M, N, L.SD_W_CONV3, cl.cin, self.grads[cl.w_key], cl.name)
 
@@ -1160,9 +1178,13 @@ class UNetEngine:
         Hl, Wl = ws.H >> u.level, ws.W >> u.level
         P = ws.B * Hh * Wh
         rows_ld = getattr(self, "_up_bias_rows", None)
-        if rows_ld is not None:  # left in t["stats"] by the decoder dgrad that produced du (_conv_bwd)
-            L.call("sd_stat_rows_sum", t["stats"].data_ptr(), rows_ld[0], rows_ld[1], u.cout,
-                   self.grads[u.name + ".bias"].data_ptr(), s)
+        if rows_ld is not None:  # left by the decoder dgrad that produced du (_conv_bwd, _bias_rows_ptr)
+            rows, ld, ptr = rows_ld
+            bias = self.grads[u.name + ".bias"].data_ptr()
+            if self.defer_reduce:
+                self._red_jobs.append(L.SdWredJob(ptr, rows, 1, ld, L.SD_W_ROWSUM, u.cout, bias))
+            else:
+                L.call("sd_stat_rows_sum", ptr, rows, ld, u.cout, bias, s)
             self._up_bias_rows = None
         else:
             L.call("sd_chan_sum", dt, du.data_ptr(), P, u.cout, t["chan"].data_ptr(),

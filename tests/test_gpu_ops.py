@@ -163,6 +163,14 @@ def test_conv3x3_dual_source_and_dgrad_split(prec, B, H, W, c0, c1, co):
         lib.call("sd_stat_rows_sum", st.data_ptr(), rows, N, c0, bias_grad.data_ptr(), lib.stream_handle())
         ref_sum = du.double().sum(0).float()
         assert torch.allclose(bias_grad, ref_sum, rtol=1e-4, atol=1e-3)
+        # the same sums as an SD_W_ROWSUM job of the batched reduce, beside a weight-gradient job: bit-identical
+        slab = torch.randn(3, 8, 9 * 8, device=DEV)
+        dw_one, dw_bat, bias_bat = torch.empty(8, 8, 9, device=DEV), torch.empty(8, 8, 9, device=DEV), torch.empty(c0, device=DEV)
+        lib.call("sd_wgrad_reduce", slab.data_ptr(), 3, 8, 72, lib.SD_W_CONV3, 8, dw_one.data_ptr(), lib.stream_handle())
+        jobs = (lib.SdWredJob * 2)(lib.SdWredJob(slab.data_ptr(), 3, 8, 72, lib.SD_W_CONV3, 8, dw_bat.data_ptr()),
+                                   lib.SdWredJob(st.data_ptr(), rows, 1, N, lib.SD_W_ROWSUM, c0, bias_bat.data_ptr()))
+        lib.call("sd_wgrad_reduce_batch", jobs, 2, lib.stream_handle())
+        assert torch.equal(bias_bat, bias_grad) and torch.equal(dw_bat, dw_one)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])

@@ -58,6 +58,11 @@ def test_host_validation_rejects_bad_args_without_launch():
         L.call("sd_pool_bwd_add", L.SD_F32, 1, 1, 1, None, 1, 1, 7, 8, 8, 1, None, None, None, None)
     with pytest.raises(L.StereoHipError, match="kpad"):
         L.call("sd_pack_conv3_w", L.SD_F32, 1, 32, 32, 32, 0, 100, 1, None)
+    # row-sum jobs of the batched reduce (the ConvTranspose bias gradients): M = 1, C <= pitch, 8-B aligned rows
+    for M, N, C, ptr in ((2, 64, 32, 16), (1, 16, 32, 16), (1, 64, 32, 20)):
+        jobs = (L.SdWredJob * 1)(L.SdWredJob(ptr, 4, M, N, L.SD_W_ROWSUM, C, 16))
+        with pytest.raises(L.StereoHipError, match="row-sum job 0"):
+            L.call("sd_wgrad_reduce_batch", jobs, 1, None)
 
 
 def test_planning_queries_are_host_only():
