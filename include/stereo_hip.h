@@ -272,6 +272,12 @@ int sd_stat_rows_sum(const float* stats, int rows, int ld, int C, float* out, sd
  * clear[0..ncount-1] for the caller's next call (double-buffered counters: one launch per batch). */
 int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount, int* clear,
                    sd_stream s);
+/* the train step's prologue in ONE launch (train.py:320-330 before the forward): sd_pack_weights(dtype, jobs, njobs,
+ * wpack), sd_pack_input(dtype, x, batch, cin, H, W, cpad, xout) and sd_count_valid(target, mask, pixels, count, ncount,
+ * clear) with a non-NULL clear, a 4-B aligned mask and 16-B aligned targets; the same results as the three calls */
+int sd_step_prologue(int dtype, const sd_pack_job* jobs, int njobs, void* wpack, const float* x, int batch, int cin,
+                     int H, int W, int cpad, void* xout, const float* target, const uint8_t* mask, int64_t pixels,
+                     int* count, int ncount, int* clear, sd_stream s);
 int sd_heads_rows(int64_t pixels);
 int sd_heads(int dtype, int mode, const void* y, const float* scale, const float* shift, int64_t pixels, int C,
              const float* wd, const float* bd, const float* wl, const float* bl, float* disp, float* logvar,

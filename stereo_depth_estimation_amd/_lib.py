@@ -160,6 +160,7 @@ PROTOTYPES: dict[str, tuple] = {
     "sd_chan_sum": (_i, [_i, _p, _i64, _i, _p, _p, _p]),
     "sd_stat_rows_sum": (_i, [_p, _i, _i, _i, _p, _p]),
     "sd_count_valid": (_i, [_p, _p, _i64, _p, _i, _p, _p]),
+    "sd_step_prologue": (_i, [_i, _PJOB, _i, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i64, _p, _i, _p, _p]),
     "sd_heads_rows": (_i, [_i64]),
     "sd_heads": (_i, [_i, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "sd_heads_bnsum": (_i, [_i, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,

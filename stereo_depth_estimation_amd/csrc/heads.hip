@@ -334,59 +334,6 @@ __global__ __launch_bounds__(256) void k_heads_finalize(const float* __restrict_
     }
 }
 
-// 4 pixels per thread per iteration (one 32-bit mask word, one float4 of targets), block
-// reduction, one atomic per block
-__global__ __launch_bounds__(256) void k_count_valid(const float* __restrict__ t, const uint8_t* __restrict__ m,
-                                                     long long P, int* count, int ncount, int* clear) {
-    // clear: the other slot of the caller's double-buffered counters, zeroed for its next call (no memset launch)
-    if (clear && blockIdx.x == 0 && threadIdx.x < ncount) clear[threadIdx.x] = 0;
-    int c = 0;
-    const long long P4 = P / 4;
-    auto cnt = [](unsigned mw, float4 tv) {
-        return ((mw & 0xffu) != 0 && isfinite(tv.x)) + (((mw >> 8) & 0xffu) != 0 && isfinite(tv.y)) +
-               (((mw >> 16) & 0xffu) != 0 && isfinite(tv.z)) + ((mw >> 24) != 0 && isfinite(tv.w));
-    };
-    // four passes' loads issued together: each pass was a dependent HBM round trip (the 4.9 M pixels of a 320x240
-    // B = 64 step took 5 of them at 1024 blocks, 29 us for 25 MB)
-    const long long stride = (long long)gridDim.x * 256;
-    long long i = blockIdx.x * 256LL + threadIdx.x;
-    for (; i + 3 * stride < P4; i += 4 * stride) {
-        unsigned mw[4];
-        float4 tv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            mw[k] = reinterpret_cast<const unsigned*>(m)[i + k * stride];
-            tv[k] = reinterpret_cast<const float4*>(t)[i + k * stride];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c += cnt(mw[k], tv[k]);
-    }
-    for (; i < P4; i += stride) c += cnt(reinterpret_cast<const unsigned*>(m)[i], reinterpret_cast<const float4*>(t)[i]);
-    for (long long i = P4 * 4 + blockIdx.x * 256LL + threadIdx.x; i < P; i += (long long)gridDim.x * 256)
-        c += (m[i] != 0 && isfinite(t[i])) ? 1 : 0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    __shared__ int red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    // the counters' atomics from different lanes (they serialize per address, not across addresses)
-    if (threadIdx.x < ncount) {
-        const int s = red[0] + red[1] + red[2] + red[3];
-        if (s) atomicAdd(count + threadIdx.x, s);
-    }
-}
-
-__global__ __launch_bounds__(256) void k_count_valid_scalar(const float* __restrict__ t, const uint8_t* __restrict__ m,
-                                                            long long P, int* count, int ncount) {
-    int c = 0;
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < P; i += (long long)gridDim.x * 256)
-        c += (m[i] != 0 && isfinite(t[i])) ? 1 : 0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if ((threadIdx.x & 63) == 0 && c)
-        for (int k = 0; k < ncount; ++k) atomicAdd(count + k, c);
-}
-
 int heads_rows(long long P) {
     long long r = (P + 255) / 256;
     return (int)(r > 1024 ? 1024 : (r < 1 ? 1 : r));
@@ -426,27 +373,6 @@ int launch_heads(int C, int mode, const void* y, const float* sc, const float* s
 }
 
 }  // namespace
-
-extern "C" int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount,
-                              int* clear, sd_stream s) {
-    SD_REQUIRE(target && mask && count && pixels > 0 && ncount >= 1 && ncount <= 4, "sd_count_valid: bad args");
-    SD_REQUIRE(!clear || clear + ncount <= count || count + ncount <= clear, "sd_count_valid: clear overlaps count");
-    if (!clear && hipMemsetAsync(count, 0, sizeof(int) * ncount, to_stream(s)) != hipSuccess)
-        return sd_check_launch("sd_count_valid");
-    // one atomic per block and counter, and the same-address atomics serialize (1024 blocks x 2 counters took ~28 us
-    // at 320x240 B=64): 256 blocks, each thread with ~18 16-B target loads in passes of four
-    long long g = (pixels / 4 + 255) / 256;
-    if (g > 256) g = 256;
-    if (g < 1) g = 1;
-    // the vector path needs a 4-B aligned mask and 16-B aligned targets; otherwise scalar-only
-    const bool vec = ((uintptr_t)mask % 4 == 0) && ((uintptr_t)target % 16 == 0);
-    hipLaunchKernelGGL(k_count_valid, dim3((int)g), dim3(256), 0, to_stream(s), target, mask,
-                       vec ? (long long)pixels : 0LL, count, ncount, clear);
-    if (!vec)
-        hipLaunchKernelGGL(k_count_valid_scalar, dim3((int)g), dim3(256), 0, to_stream(s), target, mask,
-                           (long long)pixels, count, ncount);
-    return sd_check_launch("sd_count_valid");
-}
 
 extern "C" int sd_heads_rows(int64_t pixels) { return heads_rows(pixels); }
 

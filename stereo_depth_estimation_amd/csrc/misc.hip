@@ -77,10 +77,11 @@ namespace {
 // one pixel per thread: coalesced plane reads (consecutive threads, consecutive pixels), one 8-channel
 // vector store per 8 output channels
 template <typename T>
-__global__ void k_pack_input(const float* __restrict__ x, int batch, int cin, int H, int W, int cpad, T* out) {
+__device__ __forceinline__ void pack_input_blocks(const float* __restrict__ x, int batch, int cin, int H, int W, int cpad,
+                                                  T* out, int bid, int nblk) {
     const long long P = (long long)batch * H * W;
     const long long hw = (long long)H * W;
-    for (long long px = blockIdx.x * 256LL + threadIdx.x; px < P; px += (long long)gridDim.x * 256) {
+    for (long long px = bid * 256LL + threadIdx.x; px < P; px += (long long)nblk * 256) {
         const long long b = px / hw, r = px - b * hw;
         const float* src = x + b * cin * hw + r;
         for (int c0 = 0; c0 < cpad; c0 += 8) {
@@ -90,6 +91,10 @@ __global__ void k_pack_input(const float* __restrict__ x, int batch, int cin, in
             store8(out + px * cpad + c0, v);
         }
     }
+}
+template <typename T>
+__global__ void k_pack_input(const float* __restrict__ x, int batch, int cin, int H, int W, int cpad, T* out) {
+    pack_input_blocks(x, batch, cin, H, W, cpad, out, blockIdx.x, gridDim.x);
 }
 
 // k_pack_input that also takes max |x| over the batch (the fp8 path's input-range check, engine._fp8_policy): per-block
@@ -189,15 +194,14 @@ __device__ __forceinline__ T split_half(float v, int lo) {
     return from_f32<T>(lo ? v - hi : v);
 }
 template <typename T>
-__global__ __launch_bounds__(256) void k_pack_multi(const PackJobs P, T* __restrict__ out) {
-    __shared__ float sw[PACK_LDS_FLOATS];
-    int lo = 0, hi = P.n - 1;  // largest j with first[j] <= blockIdx.x
+__device__ __forceinline__ void pack_multi_block(const PackJobs& P, T* __restrict__ out, int bid, float* sw) {
+    int lo = 0, hi = P.n - 1;  // largest j with first[j] <= bid
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (P.first[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+        if (P.first[mid] <= bid) lo = mid; else hi = mid - 1;
     }
     const sd_pack_job& jb = P.j[lo];
-    const int r = blockIdx.x - P.first[lo];  // row (group) of this block
+    const int r = bid - P.first[lo];  // row (group) of this block
     const int tid = threadIdx.x;
     T* o = out + jb.out_off;
     const int co = jb.co, ci = jb.ci;
@@ -269,6 +273,92 @@ __global__ __launch_bounds__(256) void k_pack_multi(const PackJobs P, T* __restr
             }
         }
     }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_multi(const PackJobs P, T* __restrict__ out) {
+    __shared__ float sw[PACK_LDS_FLOATS];
+    pack_multi_block(P, out, blockIdx.x, sw);
+}
+
+// ------------------------------------------------------------------ valid-pixel count (train.py:329-330)
+// 4 pixels per thread per iteration (one 32-bit mask word, one float4 of targets), block reduction, one atomic per
+// block and counter
+__device__ __forceinline__ void count_valid_blocks(const float* __restrict__ t, const uint8_t* __restrict__ m,
+                                                   long long P, int* count, int ncount, int* clear, int bid, int nblk) {
+    // clear: the other slot of the caller's double-buffered counters, zeroed for its next call (no memset launch)
+    if (clear && bid == 0 && threadIdx.x < ncount) clear[threadIdx.x] = 0;
+    int c = 0;
+    const long long P4 = P / 4;
+    auto cnt = [](unsigned mw, float4 tv) {
+        return ((mw & 0xffu) != 0 && isfinite(tv.x)) + (((mw >> 8) & 0xffu) != 0 && isfinite(tv.y)) +
+               (((mw >> 16) & 0xffu) != 0 && isfinite(tv.z)) + ((mw >> 24) != 0 && isfinite(tv.w));
+    };
+    // four passes' loads issued together: each pass was a dependent HBM round trip (the 4.9 M pixels of a 320x240
+    // B = 64 step took 5 of them at 1024 blocks, 29 us for 25 MB)
+    const long long stride = (long long)nblk * 256;
+    long long i = bid * 256LL + threadIdx.x;
+    for (; i + 3 * stride < P4; i += 4 * stride) {
+        unsigned mw[4];
+        float4 tv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mw[k] = reinterpret_cast<const unsigned*>(m)[i + k * stride];
+            tv[k] = reinterpret_cast<const float4*>(t)[i + k * stride];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c += cnt(mw[k], tv[k]);
+    }
+    for (; i < P4; i += stride) c += cnt(reinterpret_cast<const unsigned*>(m)[i], reinterpret_cast<const float4*>(t)[i]);
+    for (long long i = P4 * 4 + bid * 256LL + threadIdx.x; i < P; i += (long long)nblk * 256)
+        c += (m[i] != 0 && isfinite(t[i])) ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    __shared__ int red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    // the counters' atomics from different lanes (they serialize per address, not across addresses)
+    if (threadIdx.x < ncount) {
+        const int s = red[0] + red[1] + red[2] + red[3];
+        if (s) atomicAdd(count + threadIdx.x, s);
+    }
+}
+__global__ __launch_bounds__(256) void k_count_valid(const float* __restrict__ t, const uint8_t* __restrict__ m,
+                                                     long long P, int* count, int ncount, int* clear) {
+    count_valid_blocks(t, m, P, count, ncount, clear, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(256) void k_count_valid_scalar(const float* __restrict__ t, const uint8_t* __restrict__ m,
+                                                            long long P, int* count, int ncount) {
+    int c = 0;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < P; i += (long long)gridDim.x * 256)
+        c += (m[i] != 0 && isfinite(t[i])) ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c)
+        for (int k = 0; k < ncount; ++k) atomicAdd(count + k, c);
+}
+
+// ------------------------------------------------------------------ the train step's prologue in one launch
+// blocks [0, nb_cnt): the valid count (latency-bound: dispatched first), [nb_cnt, nb_cnt + nb_pack): the weight packs,
+// the rest: the input pack (HBM-bound); three independent jobs whose launches were three kernel boundaries
+template <typename T>
+__global__ __launch_bounds__(256) void k_step_prologue(const PackJobs P, T* __restrict__ wout, int nb_pack,
+                                                       const float* __restrict__ x, int batch, int cin, int H, int W,
+                                                       int cpad, T* __restrict__ xout, int nb_in,
+                                                       const float* __restrict__ t, const uint8_t* __restrict__ m,
+                                                       long long pixels, int* count, int ncount, int* clear,
+                                                       int nb_cnt) {
+    __shared__ float sw[PACK_LDS_FLOATS];
+    int b = blockIdx.x;
+    if (b < nb_cnt) {
+        count_valid_blocks(t, m, pixels, count, ncount, clear, b, nb_cnt);
+        return;
+    }
+    b -= nb_cnt;
+    if (b < nb_pack) {
+        pack_multi_block(P, wout, b, sw);
+        return;
+    }
+    pack_input_blocks(x, batch, cin, H, W, cpad, xout, b - nb_pack, nb_in);
 }
 
 // ------------------------------------------------------------------ AdamW
@@ -411,12 +501,12 @@ extern "C" int sd_pack_convT_w(int dtype, const float* w, int ci, int co, int dg
     return sd_check_launch("sd_pack_convT_w");
 }
 
-extern "C" int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, void* out, sd_stream s) {
-    SD_REQUIRE(jobs && out && njobs > 0 && njobs <= PACK_MAX_JOBS, "sd_pack_weights: njobs=%d (max %d)", njobs,
+// validation and block ranges of a pack job table (sd_pack_weights, sd_step_prologue)
+static int pack_plan(int dtype, const sd_pack_job* jobs, int njobs, PackJobs& P, long long& blocks) {
+    SD_REQUIRE(jobs && njobs > 0 && njobs <= PACK_MAX_JOBS, "sd_pack_weights: njobs=%d (max %d)", njobs,
                PACK_MAX_JOBS);
-    PackJobs P;
     P.n = njobs;
-    long long blocks = 0;
+    blocks = 0;
     for (int j = 0; j < njobs; ++j) {
         const sd_pack_job& q = jobs[j];
         SD_REQUIRE(q.w && q.kind >= SD_PACK_CONV3_FWD && q.kind <= SD_PACK_CONVT_FWD_SPLIT && q.co > 0 && q.ci > 0 &&
@@ -461,11 +551,73 @@ extern "C" int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, vo
         SD_REQUIRE(blocks < (1LL << 30), "sd_pack_weights: too large");
     }
     P.first[njobs] = (int)blocks;
+    return 0;
+}
+
+extern "C" int sd_pack_weights(int dtype, const sd_pack_job* jobs, int njobs, void* out, sd_stream s) {
+    SD_REQUIRE(out, "sd_pack_weights: null output");
+    PackJobs P;
+    long long blocks = 0;
+    if (int e = pack_plan(dtype, jobs, njobs, P, blocks)) return e;
     if (dtype == SD_BF16)
         hipLaunchKernelGGL(k_pack_multi<__bf16>, dim3((unsigned)blocks), dim3(256), 0, to_stream(s), P, (__bf16*)out);
     else
         hipLaunchKernelGGL(k_pack_multi<float>, dim3((unsigned)blocks), dim3(256), 0, to_stream(s), P, (float*)out);
     return sd_check_launch("sd_pack_weights");
+}
+
+static int count_grid(long long pixels) {
+    // one atomic per block and counter, and the same-address atomics serialize (1024 blocks x 2 counters took ~28 us
+    // at 320x240 B=64): 256 blocks, each thread with ~18 16-B target loads in passes of four
+    long long g = (pixels / 4 + 255) / 256;
+    if (g > 256) g = 256;
+    return (int)(g < 1 ? 1 : g);
+}
+
+extern "C" int sd_count_valid(const float* target, const uint8_t* mask, int64_t pixels, int* count, int ncount,
+                              int* clear, sd_stream s) {
+    SD_REQUIRE(target && mask && count && pixels > 0 && ncount >= 1 && ncount <= 4, "sd_count_valid: bad args");
+    SD_REQUIRE(!clear || clear + ncount <= count || count + ncount <= clear, "sd_count_valid: clear overlaps count");
+    if (!clear && hipMemsetAsync(count, 0, sizeof(int) * ncount, to_stream(s)) != hipSuccess)
+        return sd_check_launch("sd_count_valid");
+    const int g = count_grid(pixels);
+    // the vector path needs a 4-B aligned mask and 16-B aligned targets; otherwise scalar-only
+    const bool vec = ((uintptr_t)mask % 4 == 0) && ((uintptr_t)target % 16 == 0);
+    hipLaunchKernelGGL(k_count_valid, dim3(g), dim3(256), 0, to_stream(s), target, mask, vec ? (long long)pixels : 0LL,
+                       count, ncount, clear);
+    if (!vec)
+        hipLaunchKernelGGL(k_count_valid_scalar, dim3(g), dim3(256), 0, to_stream(s), target, mask, (long long)pixels,
+                           count, ncount);
+    return sd_check_launch("sd_count_valid");
+}
+
+extern "C" int sd_step_prologue(int dtype, const sd_pack_job* jobs, int njobs, void* wpack, const float* x, int batch,
+                                int cin, int H, int W, int cpad, void* xout, const float* target, const uint8_t* mask,
+                                int64_t pixels, int* count, int ncount, int* clear, sd_stream s) {
+    SD_REQUIRE(dtype == SD_BF16 || dtype == SD_F32, "sd_step_prologue: dtype %d", dtype);
+    SD_REQUIRE(wpack, "sd_step_prologue: null weight pack");
+    SD_REQUIRE(x && xout && batch > 0 && cin > 0 && H > 0 && W > 0 && cpad >= cin && cpad % 8 == 0,
+               "sd_step_prologue: bad input pack args");
+    SD_REQUIRE(target && mask && count && clear && pixels > 0 && ncount >= 1 && ncount <= 4 &&
+                   (clear + ncount <= count || count + ncount <= clear),
+               "sd_step_prologue: bad count args");
+    SD_REQUIRE((uintptr_t)mask % 4 == 0 && (uintptr_t)target % 16 == 0,
+               "sd_step_prologue: the count needs a 4-B aligned mask and 16-B aligned targets (use sd_count_valid)");
+    PackJobs P;
+    long long nb_pack = 0;
+    if (int e = pack_plan(dtype, jobs, njobs, P, nb_pack)) return e;
+    const int nb_cnt = count_grid(pixels), nb_in = grid_for((long long)batch * H * W);
+    const long long blocks = nb_pack + nb_cnt + nb_in;
+    SD_REQUIRE(blocks < (1LL << 30), "sd_step_prologue: too large");
+    if (dtype == SD_BF16)
+        hipLaunchKernelGGL(k_step_prologue<__bf16>, dim3((unsigned)blocks), dim3(256), 0, to_stream(s), P,
+                           (__bf16*)wpack, (int)nb_pack, x, batch, cin, H, W, cpad, (__bf16*)xout, nb_in, target, mask,
+                           (long long)pixels, count, ncount, clear, nb_cnt);
+    else
+        hipLaunchKernelGGL(k_step_prologue<float>, dim3((unsigned)blocks), dim3(256), 0, to_stream(s), P,
+                           (float*)wpack, (int)nb_pack, x, batch, cin, H, W, cpad, (float*)xout, nb_in, target, mask,
+                           (long long)pixels, count, ncount, clear, nb_cnt);
+    return sd_check_launch("sd_step_prologue");
 }
 
 extern "C" int sd_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double weight_decay,

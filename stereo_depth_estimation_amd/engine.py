@@ -232,6 +232,9 @@ class UNetEngine:
         # (sd_conv3x3_bwd_fused / _dec: dy stays in LDS; SD_BWD_FUSE=0: weight gradient + dgrad launches;
         # SD_BWD_FUSE=1: the conv1 layers only)
         self.bwd_fuse = {"0": 0, "1": 1}.get(os.environ.get("SD_BWD_FUSE", "2"), 2)
+        # train step: the valid count, the weight packs and the input pack in one launch (step_prologue;
+        # SD_PROLOGUE=0: three launches)
+        self.prologue = os.environ.get("SD_PROLOGUE", "1") != "0"
         self._bnsum_rows: dict[str, int] = {}
         # training: the split-K slab reduce of every weight gradient on a second stream (SD_SIDE_REDUCE=1), so it
         # overlaps the next layer's kernels instead of adding a kernel boundary to the critical path; 2: the
@@ -312,6 +315,15 @@ class UNetEngine:
                 L.call("sd_pack_weights", L.SD_BF16, arr, len(jobs), self.wsplit_pack.data_ptr(), s)
             return
         # every bf16/fp32 pack of the step in one launch (job table rebuilt when the parameters move)
+        jobs = self._pack_table()
+        L.call("sd_pack_weights", dt, jobs, len(jobs), base, s)
+        if self._split_pack_jobs is not None and (not train or self.wsplit_train):
+            L.call("sd_pack_weights", L.SD_BF16, self._split_pack_jobs, len(self._split_pack_jobs),
+                   self.wsplit_pack.data_ptr(), s)
+
+    def _pack_table(self):
+        """The bf16/fp32 sd_pack_weights job table of every layer (and the split-pack table), rebuilt when the
+        parameters move."""
         key = tuple(t.data_ptr() for t in self.params.values())
         if getattr(self, "_pack_key", None) != key:
             jobs = []
@@ -328,10 +340,32 @@ class UNetEngine:
             sj = self._split_jobs()
             self._split_pack_jobs = (L.SdPackJob * len(sj))(*[L.SdPackJob(*j) for j in sj]) if sj else None
             self._pack_key = key
-        L.call("sd_pack_weights", dt, self._pack_jobs, len(self._pack_jobs), base, s)
+        return self._pack_jobs
+
+    def step_prologue(self, x: torch.Tensor, target: torch.Tensor, valid: torch.Tensor, train: bool) -> bool:
+        """count_valid(target, valid) + pack_weights(train=train) + the next forward(x)'s input pack as ONE launch
+        (sd_step_prologue: three independent jobs that were three kernel boundaries). Returns False, having launched
+        nothing, where it does not apply (the fp8 forward, SD_PROLOGUE=0, an input that is not a contiguous fp32 NCHW
+        batch of this model, targets or mask not aligned for the vector count): the caller then makes the three
+        calls."""
+        if (self.fp8 or not self.prologue or x.dim() != 4 or x.shape[1] != self.in_channels or not x.is_contiguous()
+                or x.dtype != torch.float32 or x.shape[2] % 16 or x.shape[3] % 16 or target.data_ptr() % 16
+                or valid.data_ptr() % 4 or target.numel() != valid.numel()):
+            return False
+        B, C, H, W = x.shape
+        ws = self.workspace(B, H, W, train)
+        k = self._count_slot()
+        jobs = self._pack_table()
+        s = self._s()
+        self._packed_key = None
+        L.call("sd_step_prologue", self.sd_dtype, jobs, len(jobs), self.wpack.data_ptr(), x.data_ptr(), B, C, H, W,
+               self.cin_pad0, ws.t["xin"].data_ptr(), target.data_ptr(), valid.data_ptr(), target.numel(),
+               self._counts[k].data_ptr(), 2, self._counts[k ^ 1].data_ptr(), s)
         if self._split_pack_jobs is not None and (not train or self.wsplit_train):
             L.call("sd_pack_weights", L.SD_BF16, self._split_pack_jobs, len(self._split_pack_jobs),
                    self.wsplit_pack.data_ptr(), s)
+        self._xin_ready = (x.data_ptr(), tuple(x.shape), ws.t["xin"].data_ptr())
+        return True
 
     def _split_jobs(self) -> list:
         """sd_pack_weights jobs of the hi/lo split weights (wsplit layers)."""
@@ -749,7 +783,10 @@ class UNetEngine:
             ws.coeff_key = key
         self.phase = "fwd"  # read by measurement hooks (bench.py) to tell forward from backward launches
         x = x.contiguous().float()
-        if self.fp8 and self.fp8_static and self._q8_shapes:
+        ready, self._xin_ready = getattr(self, "_xin_ready", None), None
+        if ready is not None and ready == (x.data_ptr(), tuple(x.shape), ws.t["xin"].data_ptr()):
+            pass  # packed by step_prologue
+        elif self.fp8 and self.fp8_static and self._q8_shapes:
             self._pack_input_fp8(ws, x)
         else:
             L.call("sd_pack_input", self.sd_dtype, x.data_ptr(), B, C, H, W, self.cin_pad0, ws.t["xin"].data_ptr(),
@@ -944,12 +981,17 @@ class UNetEngine:
     def count_valid(self, target: torch.Tensor, valid: torch.Tensor):
         """train.py:329-330 valid count, on device: count_local (this rank's pixels, for the
         metric sums) and count (the loss normaliser; DDP all-reduces it to the global count)."""
+        k = self._count_slot()
+        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts[k].data_ptr(), 2,
+               self._counts[k ^ 1].data_ptr(), self._s())
+
+    def _count_slot(self) -> int:
+        """The double-buffered counter pair this batch counts into (count_local / count point at it)."""
         k = self._cslot
         self._cslot ^= 1
         self.count_local = self._counts[k, 0:1]
         self.count = self._counts[k, 1:2]
-        L.call("sd_count_valid", target.data_ptr(), valid.data_ptr(), target.numel(), self._counts[k].data_ptr(), 2,
-               self._counts[k ^ 1].data_ptr(), self._s())
+        return k
 
     # ------------------------------------------------------------------ backward
     @staticmethod

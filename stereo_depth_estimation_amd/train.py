@@ -59,9 +59,14 @@ def _train_step(model, eng, optimizer, inputs, targets, valid_mask, grad_hook, c
     training = optimizer is not None
     mask_u8 = valid_mask.contiguous().view(torch.uint8)
     targets = targets.contiguous()
-    eng.count_valid(targets, mask_u8)  # depends on the batch only: counted (and all-reduced) ahead of the forward
+    # the valid count depends on the batch only: counted (and all-reduced) ahead of the forward; with the weight packs
+    # and the input pack in one launch where it applies
+    fused = eng.step_prologue(inputs, targets, mask_u8, training)
+    if not fused:
+        eng.count_valid(targets, mask_u8)
     pending = count_hook(eng.count) if count_hook is not None else None
-    eng.pack_weights(train=training)
+    if not fused:
+        eng.pack_weights(train=training)
     eng.forward(inputs, train=training)
     if pending is not None:
         pending.wait()

@@ -241,6 +241,33 @@ def test_deferred_slab_reduces_bit_identical(monkeypatch, precision):
         assert torch.equal(p0, runs["1"][2][k]), k
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_step_prologue_bit_identical(monkeypatch, precision):
+    """The train step's valid count, weight packs and input pack in one sd_step_prologue launch (default) give exactly
+    the gradients, metrics and updated weights of the three launches (SD_PROLOGUE=0), and the skipped-step gate still
+    sees the count (an all-invalid batch leaves the weights and the step counter alone)."""
+    st = U.make_state(32, seed=4)
+    bs = [U.make_batch(2, 64, 96, seed=8), U.make_batch(2, 64, 96, seed=9), U.make_batch(2, 64, 96, seed=10)]
+    bs[2]["valid_mask"][:] = False
+    runs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SD_PROLOGUE", mode)
+        m, metrics, _, grads = _fused_two_steps(st, 32, precision, bs)
+        assert m.engine().prologue == (mode == "1")
+        torch.cuda.synchronize()
+        runs[mode] = (metrics, grads, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                      int(m.engine().adam_step.item()))
+    assert runs["1"][3] == runs["0"][3] == 2
+    assert runs["0"][0].keys() == runs["1"][0].keys()
+    for k, a in runs["0"][0].items():
+        b = runs["1"][0][k]
+        assert a == b or (a != a and b != b), (k, a, b)
+    for k, g0 in runs["0"][1].items():
+        assert torch.equal(g0, runs["1"][1][k]), k
+    for k, p0 in runs["0"][2].items():
+        assert torch.equal(p0, runs["1"][2][k]), k
+
+
 def test_autograd_path_matches_fused_path():
     """model(x) + external loss + loss.backward() (the reference's train.py:328-342 as written)."""
     st = U.make_state(8, seed=0, signed_gamma=True)
