@@ -1,4 +1,5 @@
-"""Per-step GPU busy time from a rocprofv3 kernel trace of bench.py (steps delimited by k_pack_multi).
+"""Per-step GPU busy time from a rocprofv3 kernel trace of bench.py (steps delimited by the step prologue:
+k_step_prologue, or k_pack_multi in traces of builds before it / SD_PROLOGUE=0).
 
     python tools/step_busy.py gpurun_out/<tag>/prof/run_kernel_trace.csv [...]
 """
@@ -10,7 +11,9 @@ import sys
 def step_busy(path):
     rows = list(csv.DictReader(open(path)))
     names = [r["Kernel_Name"] for r in rows]
-    idx = [i for i, n in enumerate(names) if "k_pack_multi" in n]
+    idx = [i for i, n in enumerate(names) if "k_step_prologue" in n]
+    if len(idx) < 6:
+        idx = [i for i, n in enumerate(names) if "k_pack_multi" in n]
     busy, wall = [], []
     for a, b in zip(idx[3:-2], idx[4:-1]):  # regular training steps (skip warmup and the tail)
         busy.append(sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b]) / 1e3)
