@@ -64,7 +64,11 @@ def _train_step(model, eng, optimizer, inputs, targets, valid_mask, grad_hook, c
     fused = eng.step_prologue(inputs, targets, mask_u8, training)
     if not fused:
         eng.count_valid(targets, mask_u8)
-    pending = count_hook(eng.count) if count_hook is not None else None
+    try:
+        pending = count_hook(eng.count) if count_hook is not None else None
+    except BaseException:
+        eng._xin_ready = None  # the packed input belongs to this step's forward only
+        raise
     if not fused:
         eng.pack_weights(train=training)
     eng.forward(inputs, train=training)
