@@ -225,6 +225,60 @@ class GemmTimer:
                  "ms_per_step": ms / steps} for ms, k, n, fl, by in rows]
 
 
+def conv_layers(H: int = 240, W: int = 320, base: int = 32, cin: int = 6):
+    """The U-Net's GEMM-shaped layers (model.py:61-77): (name, kind, cin, cout, out_h, out_w, in_h, in_w); kind conv3
+    (3x3, pad 1), convT (2x2 stride 2: in_h x in_w -> out), head (the two 1x1 heads as one 32 -> 2 GEMM)."""
+    ch = [base, 2 * base, 4 * base, 8 * base, 16 * base]
+    L = []
+    c = cin
+    for i, blk in enumerate(("enc1", "enc2", "enc3", "enc4", "bottleneck")):
+        h, w = H >> i, W >> i
+        L += [(blk + ".0", "conv3", c, ch[i], h, w, h, w), (blk + ".1", "conv3", ch[i], ch[i], h, w, h, w)]
+        c = ch[i]
+    for i, (up, dec) in zip((3, 2, 1, 0), (("up4", "dec4"), ("up3", "dec3"), ("up2", "dec2"), ("up1", "dec1"))):
+        h, w = H >> i, W >> i
+        L += [(up, "convT", ch[i + 1], ch[i], h, w, h // 2, w // 2),
+              (dec + ".0", "conv3", 2 * ch[i], ch[i], h, w, h, w), (dec + ".1", "conv3", ch[i], ch[i], h, w, h, w)]
+    L.append(("heads", "head", base, 2, H, W, H, W))
+    return L
+
+
+def step_roofline(ms_per_step: float | None, B: int = 64, H: int = 240, W: int = 320, peak_tflops: float = 2500.0,
+                  hbm_gbs: float = 8000.0):
+    """SURVEY §8d's whole-step conv roofline: for every conv3x3 / ConvTranspose2d / head GEMM of the training step and
+    each of its forward, dgrad (not enc1.0's: the input needs no gradient) and weight gradient, the attainable time
+    max(FLOPs / peak, algorithmic bytes / HBM); frac = that sum / the measured ms per step. Algorithmic bytes (bf16
+    activations, minimal): fwd reads the input once, writes the output once, reads the weights; dgrad reads dy and the
+    weights, writes dx; wgrad reads x and dy, writes the fp32 dW. FLOPs = 2 MACs with real channel counts (85.025
+    GFLOP per pair at 320x240)."""
+    rows, t_att, fl_tot = {}, 0.0, 0.0
+    for name, kind, ci, co, h, w, hi, wi in conv_layers(H, W):
+        px_o, px_i = B * h * w, B * hi * wi
+        k = 9 if kind == "conv3" else 1
+        wts = k * ci * co * (4 if kind == "convT" else 1)
+        macs = px_o * co * ci * k if kind != "convT" else px_i * ci * 4 * co
+        x_b, y_b = 2.0 * px_i * ci, 2.0 * px_o * co
+        ops = {"fwd": (2.0 * macs, x_b + y_b + 2.0 * wts), "wgrad": (2.0 * macs, x_b + y_b + 4.0 * wts)}
+        if name != "enc1.0":
+            ops["dgrad"] = (2.0 * macs, y_b + x_b + 2.0 * wts)
+        r = {}
+        for op, (fl, by) in ops.items():
+            t_f, t_b = fl / (peak_tflops * 1e12), by / (hbm_gbs * 1e9)
+            r[op] = [round(max(t_f, t_b) * 1e6, 2), "mfma" if t_f >= t_b else "hbm"]
+            t_att += max(t_f, t_b)
+            fl_tot += fl
+        rows[name] = r
+    res = {"attainable_ms_per_step": round(t_att * 1e3, 4), "gflop_per_pair": round(fl_tot / B / 1e9, 3),
+           "ceiling_pairs_s": round(B / t_att, 1), "peak_tflops": peak_tflops, "hbm_gbs": hbm_gbs,
+           "definition": "sum over conv3x3/ConvTranspose2d/head GEMMs x {fwd, dgrad, wgrad} of max(FLOPs/peak, "
+                         "algorithmic bytes/HBM) at this batch, divided by the measured ms per step (SURVEY §8d)",
+           "layers_us": rows}
+    if ms_per_step:
+        res["measured_ms_per_step"] = round(ms_per_step, 4)
+        res["frac"] = round(t_att * 1e3 / ms_per_step, 4)
+    return res
+
+
 def lib_sha256() -> str:
     import hashlib
 
@@ -282,6 +336,9 @@ def epe_block(torch, model, opt, dev, steps: int):
     with torch.no_grad():
         d16, d32 = model(val[0]["input"]), ref(val[0]["input"])
     vmask = val[0]["valid_mask"]
+    # for cpu_autocast_bound (the cpu_baseline leg): the same pairs and weights on the host
+    epe_block.held = {"x": val[0]["input"].cpu(), "state": {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()},
+                      "d16": d16.float().cpu(), "d32": d32.float().cpu()}
     res = {"train_steps": steps, "train_s": round(t_train, 2), "eval_pairs": 128,
            "epe_bf16": round(m16["mae"], 6), "epe_fp32": round(m32["mae"], 6),
            "delta": round(abs(m16["mae"] - m32["mae"]), 6), "target": 1e-3,
@@ -384,6 +441,38 @@ def cpu_baseline(seconds: float, height: int, width: int):
     dt = time.perf_counter() - t0
     return {"value": n * bsz / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
             "sample": f"{n} train steps x {bsz} pairs @{width}x{height} fp32 (oracle restatement of train.py:320-343)"}
+
+
+def cpu_autocast_bound(held: dict, chunk: int = 8):
+    """The checker of epe.per_pixel_bf16_vs_fp32, run on the host in the cpu_baseline leg: the
+    reference's own bf16 behaviour on the bench model's weights and validation pairs — the oracle's eval forward under
+    torch.autocast("cpu", bfloat16) against its fp32 forward (model.py:79-104; the yardstick of tests/test_gpu_configs.py)
+    — beside the HIP bf16 path's deviation from the HIP fp32 path on the same pairs (and the HIP fp32 path's from the
+    oracle's fp32, which the tests hold within 1e-3)."""
+    import torch
+
+    from oracle import unet_ref as U
+
+    t0 = time.perf_counter()
+    net = U.Net(held["state"])
+    x = held["x"]
+    d32s, dacs = [], []
+    with torch.no_grad():
+        for i in range(0, x.shape[0], chunk):
+            xb = x[i:i + chunk]
+            d32s.append(net.forward(xb, train=False)[0])
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                dacs.append(net.forward(xb, train=False)[0].float())
+    o32, oac = torch.cat(d32s), torch.cat(dacs)
+    dev_ac = (oac - o32).abs()
+    dev16 = (held["d16"] - held["d32"]).abs()
+    flat = int(dev16.flatten().argmax())
+    return {"pairs": int(x.shape[0]), "hip_bf16_max": round(float(dev16.max()), 5),
+            "reference_autocast_max": round(float(dev_ac.max()), 5),
+            "hip_bf16_mean": round(float(dev16.mean()), 6), "reference_autocast_mean": round(float(dev_ac.mean()), 6),
+            "reference_autocast_at_hip_worst_pixel": round(float(dev_ac.flatten()[flat]), 5),
+            "hip_fp32_vs_oracle_fp32_max": round(float((held["d32"] - o32).abs().max()), 6),
+            "within": float(dev16.max()) <= float(dev_ac.max()), "seconds": round(time.perf_counter() - t0, 1)}
 
 
 def _free_port() -> int:
@@ -576,6 +665,8 @@ def main():
     peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
     step_tflops = TRAIN_GFLOP_PER_PAIR * 1e9 * B * (H * W) / (240 * 320) / (dt / args.steps) / 1e12
     result["step_conv_tflops"] = round(step_tflops, 2)
+    if args.precision == "bf16":
+        result["step_roofline"] = step_roofline(ms_per_step, B, H, W, peak)
     if timer is not None:
         kern = timer.summary(args.steps)
         top = kern[0]
@@ -621,6 +712,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, H, W)
+        held = getattr(epe_block, "held", None)
+        if held is not None and "epe" in result:
+            log("reference autocast bound of the bf16 per-pixel deviation (oracle, host) ...")
+            result["epe"]["per_pixel_bf16_vs_fp32"]["bound"] = cpu_autocast_bound(held)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -88,6 +88,7 @@ class Workspace:
     q8_ready: bool = False  # fp8: the activation scales of a calibration forward are in t
     graph: object = None  # HIP graph of the eval forward (after the input pack) for graph_key = (state key, path)
     graph_key: object = None
+    graph_zs: frozenset = frozenset()  # the layers whose stored output the captured body BN-applied (engine._zs)
 
 
 class UNetEngine:
@@ -461,6 +462,8 @@ class UNetEngine:
                 t["dy:" + cl.name] = act(lv, cl.cout)
                 t["coef:" + cl.name] = torch.empty(cl.cout, 3, dtype=f32, device=dev)
                 max_chan = max(max_chan, L.call("sd_chan_reduce_rows", P, cl.cout) * cl.cout * 2)
+                if self._bwd_fused(cl, H, W) == 1:  # sd_conv3x3_bwd_fused: splits x 32 (sum, sum*xhat) partials
+                    max_chan = max(max_chan, L.call("sd_conv3x3_bwd_fused_splits", B, H >> lv, W >> lv) * 32 * 2)
                 sp = self._conv_splits(cl, B, H, W)
                 max_slab = max(max_slab, sp * cl.cout * 9 * cl.cin_pad)
             for u in self.ups.values():
@@ -800,6 +803,9 @@ class UNetEngine:
             if ws.graph is not None and ws.graph_key == gkey:
                 with torch.cuda.device(self.device):  # replays on the current stream of the engine's device
                     ws.graph.replay()
+                # the replayed body stored what the captured one did: its BN-applied (z) layers, not whatever the
+                # last eager forward on this workspace (e.g. a grad-enabled eval forward, raw y stores) left
+                self._zs = set(ws.graph_zs)
                 self._amax_readback()
                 return ws
         self._forward_body(ws, train)
@@ -824,22 +830,28 @@ class UNetEngine:
         `fp8_calibrations` counts calibration forwards. Returns whether this forward calibrates."""
         if not ws.q8_ready or self._eval_coeffs:  # new state, new workspace, or requested
             return True
+        # The host copy of ring word s is overwritten by the read-back of the next frame that takes word s, i.e. this
+        # frame's for word `slot` (frame f - 3's). A word is checked once its read-back has landed (query, no host
+        # block); only frame f - 3's word, on its last chance, is waited for — which happens only when the caller
+        # queues frames three deep. The side stream completes in order, so a landed frame implies the calibration
+        # frame before it landed too.
         if self._fp8_cal_amax is None and self._fp8_cal is not None:  # the calibration frame's amax, once it landed
             s, ev = self._fp8_cal
-            ev.synchronize()  # recorded a frame ago: normally complete already
-            self._fp8_cal_amax = float(self._amax_host[s])
-        # every earlier frame's amax is checked once: the previous frame's when its read-back has landed, the one before
-        # it (ring word `clear`, whose host copy the next frame's read-back overwrites) now, waiting for it if the
-        # caller queued frames faster than they complete (it was recorded two frames ago: normally done already)
+            if s == slot:
+                ev.synchronize()
+            if ev.query():
+                self._fp8_cal_amax = float(self._amax_host[s])
         hit = False
-        for s in ((slot + 1) % 3, (slot + 2) % 3):  # frame f - 2, then f - 1
+        for s in (slot, (slot + 1) % 3, (slot + 2) % 3):  # frames f - 3, f - 2, f - 1
             if not self._amax_used[s] or self._amax_checked[s]:
                 continue
             ev = self._amax_ev[s]
-            if s == (slot + 1) % 3:
+            if s == slot:
                 ev.synchronize()
             elif not ev.query():
                 continue
+            if self._fp8_cal_amax is None and self._fp8_cal is not None:  # landed: the calibration frame has too
+                self._fp8_cal_amax = float(self._amax_host[self._fp8_cal[0]])
             self._amax_checked[s] = True
             if (self.fp8_range_margin > 0 and self._fp8_cal_amax is not None
                     and float(self._amax_host[s]) > self.fp8_range_margin * self._fp8_cal_amax):
@@ -873,6 +885,7 @@ class UNetEngine:
             self.fp8_calibrations += 1
             self._fp8_age = 0
             self._fp8_cal_amax = None
+            self._amax_checked = [True] * 3  # earlier frames are not held against the new calibration frame's range
         main = torch.cuda.current_stream(self.device)
         if self._amax_used[clear]:
             main.wait_event(self._amax_ev[clear])
@@ -918,7 +931,7 @@ class UNetEngine:
                     raise RuntimeError("eval graph capture: launches would not go to the capture stream")
                 self._forward_body(ws, train)
             cur.wait_stream(self._capture_stream)
-        ws.graph, ws.graph_key = g, gkey
+        ws.graph, ws.graph_key, ws.graph_zs = g, gkey, frozenset(self._zs)
 
     def _fwd_path(self, ws: Workspace) -> str:
         if not self.fp8:

@@ -58,3 +58,15 @@ def test_bench_world_size_mismatch_exits_nonzero():
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
     assert not r.stdout.strip()
+
+
+def test_step_roofline_prices_surveys_85_gflop_step():
+    """the whole-step conv roofline. Its GEMM table must carry the survey's
+    85.025 GFLOP per training pair at 320x240 (fwd 28.430 + dgrad 28.165 + wgrad 28.430), and the attainable time at
+    B = 64 must give the survey's ~20.6-20.9 k pairs/s ceiling; frac = attainable / measured."""
+    r = bench.step_roofline(8.0, 64, 240, 320)
+    assert abs(r["gflop_per_pair"] - 85.025) < 0.01
+    assert 20_000 < r["ceiling_pairs_s"] < 21_500
+    assert r["frac"] == round(r["attainable_ms_per_step"] / 8.0, 4)
+    assert len(r["layers_us"]) == 23 and "dgrad" not in r["layers_us"]["enc1.0"]
+    assert r["layers_us"]["dec4.0"]["wgrad"][1] == "mfma" and r["layers_us"]["dec1.1"]["fwd"][1] == "hbm"

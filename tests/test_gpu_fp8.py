@@ -312,8 +312,9 @@ def test_fp8_recalibrates_when_the_input_range_grows():
 
 def test_fp8_range_check_sees_frames_queued_without_sync():
     """the range check of a frame whose input amax had not been read back yet when the next frame was
-    queued must still happen. A caller that queues frames without synchronizing gets the recalibration at most two
-    frames after the wide frame (the ring word of frame f - 2 is checked by frame f, waiting for it if needed)."""
+    queued must still happen. A caller that queues frames without synchronizing gets the recalibration at most three
+    frames after the wide frame (earlier frames' words are only queried, never waited for; the ring word of
+    frame f - 3, whose host copy frame f's read-back overwrites, is checked by frame f, waiting for it if needed)."""
     from stereo_depth_estimation_amd.model import StereoUNet
 
     st = U.make_state(32, seed=5)
@@ -329,7 +330,8 @@ def test_fp8_range_check_sees_frames_queued_without_sync():
             m(dark)
         m(bright)  # no synchronize anywhere from here on
         m(dark)
-        m(dark)  # checks the bright frame's ring word (two frames back) at the latest
+        m(dark)
+        m(dark)  # checks the bright frame's ring word (three frames back) at the latest
         assert eng.fp8_range_recalibrations == 1 and eng.fp8_calibrations == 2, (
             eng.fp8_range_recalibrations, eng.fp8_calibrations)
         for _ in range(3):

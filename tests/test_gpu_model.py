@@ -310,9 +310,14 @@ def test_eval_mode_autograd_backward_matches_reference(precision):
     x = torch.as_tensor(b["input"]).to(DEV)
     with torch.no_grad():
         for _ in range(3):  # z stores (bf16), eval packs cached, graph captured and replayed
-            m(x, return_uncertainty=True)
+            d0, lv0 = (t.clone() for t in m(x, return_uncertainty=True))
     d2, lv2 = m(x, return_uncertainty=True)
     (d2.mean() + 0.5 * lv2.mean()).backward()
+    # a no-grad eval forward after it replays the captured graph (z stores): the heads must apply only the
+    # ReLU to dec1.1's z again, not the BatchNorm the grad-enabled forward's raw y needed (the replay restores _zs)
+    with torch.no_grad():
+        d3, lv3 = m(x, return_uncertainty=True)
+    assert torch.equal(d3, d0) and torch.equal(lv3, lv0)
     assert abs(float(d2.mean()) - float(d.mean())) < (1e-4 if precision == "fp32" else 2e-2) * abs(float(d.mean()))
     named = dict(m.named_parameters())
     errs = {}

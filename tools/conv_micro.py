@@ -97,11 +97,17 @@ def run(B, H, W, ci, co, stats, s, dev, n=20):
 WGRAD_LAYERS = [  # (H, W, dy channels M, x channels ci)
     (240, 320, 32, 32), (240, 320, 32, 64), (120, 160, 64, 32), (120, 160, 64, 64), (60, 80, 128, 128),
     (30, 40, 256, 256)]
+# the ten launches of the 64 x 64-block weight gradient in one training step (enc3.1 .. dec2.0), plus dec2.1
+WGRAD_STEP = [(60, 80, 128, 128), (30, 40, 256, 128), (30, 40, 256, 256), (15, 20, 512, 256), (15, 20, 512, 512),
+              (30, 40, 256, 512), (30, 40, 256, 256), (60, 80, 128, 256), (60, 80, 128, 128), (120, 160, 64, 128),
+              (120, 160, 64, 64)]
+WGRAD_MODES = {"mf1": {"SD_WS_MF32": "1"}, "mf0": {"SD_WS_MF32": "0"}}
 
 
-def wgrad(B, s, dev):
-    """sd_wgrad_gemm + sd_wgrad_reduce at the model's 3x3 weight-gradient shapes (bf16)."""
-    for H, W, M, ci in WGRAD_LAYERS:
+def wgrad(B, s, dev, layers=WGRAD_LAYERS, modes=("default",), rounds=1):
+    """sd_wgrad_gemm + sd_wgrad_reduce at the model's 3x3 weight-gradient shapes (bf16); modes (WGRAD_MODES keys)
+    alternate per round, the minimum time per mode is printed with each mode's max |dW - dW(first mode)|."""
+    for H, W, M, ci in layers:
         P = B * H * W
         dy = torch.randn(P, M, device=dev).to(torch.bfloat16)
         x = torch.randn(P, ci, device=dev).to(torch.bfloat16)
@@ -119,6 +125,27 @@ def wgrad(B, s, dev):
         def red():
             L.call("sd_wgrad_reduce", slab.data_ptr(), sp, M, N, L.SD_W_CONV3, ci, dw.data_ptr(), s)
 
+        if modes != ("default",):
+            flops = 2.0 * P * M * N
+            best, ref, line = {}, None, f"wgrad {H}x{W} M={M} ci={ci}:"
+            for _ in range(rounds):
+                for mode in modes:
+                    for k in ("SD_WS_MF32",):
+                        os.environ.pop(k, None)
+                    os.environ.update(WGRAD_MODES.get(mode, {}))
+                    t = _time(gemm)
+                    best[mode] = min(best.get(mode, 1e30), t)
+                    red()
+                    torch.cuda.synchronize()
+                    if ref is None:
+                        ref = dw.clone()
+                    best["d" + mode] = float((dw - ref).abs().max() / ref.abs().max())
+                    best["n" + mode] = L.kernel_name("sd_wgrad_kernel_name", L.SD_BF16, a, b, M, N)
+            for mode in modes:
+                line += (f" | {mode}: {best['n' + mode].replace('k_halo_wgrad_ws', '')} {best[mode]:7.1f} us "
+                         f"{flops / best[mode] / 1e6:6.1f} TF d={best['d' + mode]:.1e}")
+            print(line, flush=True)
+            continue
         tg, tr = _time(gemm), _time(red)
         if os.environ.get("SD_WG_DIAG"):  # per-wave cycle counters of a -DWG_EXP=1024 build
             dbg = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device=dev)
@@ -166,13 +193,13 @@ def main():
         if a.startswith("--modes="):
             modes = a.split("=", 1)[1].split(",")
     compare = "--compare" in sys.argv
-    if "--wgrad" in sys.argv:
-        wgrad(B, s, dev)
-        return
     rounds = 1
     for a in sys.argv[1:]:
         if a.startswith("--rounds="):  # modes alternate per round; the minimum time per mode is printed
             rounds = int(a.split("=", 1)[1])
+    if "--wgrad" in sys.argv or "--wgrad-step" in sys.argv:
+        wgrad(B, s, dev, WGRAD_STEP if "--wgrad-step" in sys.argv else WGRAD_LAYERS, tuple(modes), rounds)
+        return
     for H, W, ci, co, stats in LAYERS:
         flops = 2.0 * B * H * W * co * 9 * ci
         line = f"{H}x{W} {ci}->{co} {'bns ' if stats == 'bns' else 'fwd ' if stats else 'dgrd'}"
