@@ -1713,19 +1713,146 @@ constexpr int WS_PD = 5;                        // tap-steps of fragment read-ah
 // tiles carry little MFMA work and need more loads in flight; one otherwise
 __host__ __device__ constexpr int ws_blocks_per_cu(int cout, int cib) { return cout == 32 && cib == 32 ? 2 : 1; }
 
-template <int COUT, int CIB, int HP, int HR, bool BNB, bool SPAN>  // dy / x channels per block; halo pitch and
-                                                       // rows (tw+2 <= HP, th+2 <= HR); BNB: BatchNorm-backward apply
-                                                       // in the dy staging; SPAN: a block's x channels may straddle
-                                                       // the two sources of a concatenation
+// MFMA waves of the MF32 instances (64 dy x 64 x channels per block): v_mfma_f32_32x32x16_bf16, k = 16 pixels.
+// The block's output is 4 quadrants (co half, ci half) of 32 x 32 x 9 taps; wave W owns every quadrant of taps W and
+// W + 4 and quadrant W of tap 8 (co half W >> 1, ci half W & 1): 9 accumulators of 16 registers, as the 16x16x32 form's
+// 36 of 4. Per 16-pixel k-step a wave reads 2 dy fragments (both co halves, shared by its 9 MFMAs) and 5 x fragments
+// (taps W, W + 4 x both ci halves, tap 8 x its half): 7 transposed pairs per 9 MFMAs of 32 cycles, against the 16x16x32
+// form's 13 pairs per 36 MFMAs of 16 cycles — the same LDS reads per tile, with a third of the MFMA instructions, so
+// the matrix pipe holds the SIMD's issue for 8 of every 32 cycles instead of 8 of 16 and the loader wave on the same
+// SIMD (BN+ReLU of the halo) gets the rest. The wave's taps are template constants, so every fragment address is a
+// per-(k-step, pixel-half) lane base plus an immediate. Fragments (tr_pair, as k_bwd_fused32): 16-lane group g holds
+// channels 16 (g & 1) + (lane & 15) of pixels 4 (g >> 1) + {0..3, 8..11} of the k-step. The slab layout is the 16x16
+// form's: slab[split][co][tap * ctot + cc * 64 + ci].
+template <int HP, int DLD, int XLD, int DY_E, int BUF, int W>
+__device__ __forceinline__ void ws_mfma32_tiles(const HWgArgs& p, const __bf16* smem, int lane, int cc, int mb,
+                                                int split, int ntile, const unsigned (&xoff)[WS_TPX / 16][2],
+                                                unsigned aoff) {
+    constexpr int KS = WS_TPX / 16;
+    constexpr int T0 = W, T1 = W + 4, C8 = W >> 1, I8 = W & 1;
+    constexpr int TO0 = ((T0 / 3) * HP + T0 % 3) * XLD * 2, TO1 = ((T1 / 3) * HP + T1 % 3) * XLD * 2;
+    constexpr int TO8 = (2 * HP + 2) * XLD * 2 + I8 * 64;  // bytes
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    const char* lds = reinterpret_cast<const char*>(smem);
+    // Fragment reads run PD MFMA steps (step = ks * 9 + k) ahead of their first use: the k-step's two dy fragments and
+    // its two halo bases at k = 0 (two sets, by k-step parity), the x fragments at k = 0, 2, 4, 6, 8 into a ring of NB
+    // (a slot is rewritten 9 - PD > 1 steps after its first use, past its second)
+    constexpr int PD = 6, NB = 5;
+    for (int it = 0; it < ntile; ++it) {
+        __syncthreads();  // tile it is in buffer it & 1 (and the loaders may overwrite the other one)
+        const unsigned bufb = (unsigned)((it & 1) * BUF * 2);
+        unsigned abase = aoff + bufb, xbase = bufb + (unsigned)(DY_E * 2);
+        asm volatile("" : "+v"(abase), "+s"(xbase));
+        bf16x8 fa[2][2], fb[NB];
+        unsigned xc[2][2];
+        auto xfrag = [&](int ks, int off) __attribute__((always_inline)) {
+            return tr_pair(reinterpret_cast<const __bf16*>(lds + xc[ks & 1][0] + off),
+                           reinterpret_cast<const __bf16*>(lds + xc[ks & 1][1] + off));
+        };
+        // the reads first needed by step j
+        auto rd = [&](int j) __attribute__((always_inline)) {
+            const int ks = j / 9, k = j - ks * 9, s = ks & 1, b = ks * 5 + k / 2;
+            if (k == 0) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const __bf16* a0 = reinterpret_cast<const __bf16*>(lds + abase) + ks * 16 * DLD + h * 32;
+                    fa[s][h] = tr_pair(a0, a0 + 8 * DLD);
+                    xc[s][h] = xoff[ks][h] + xbase;
+                }
+                fb[b % NB] = xfrag(ks, TO0);
+            } else if (k == 2) {
+                fb[b % NB] = xfrag(ks, TO0 + 64);
+            } else if (k == 4) {
+                fb[b % NB] = xfrag(ks, TO1);
+            } else if (k == 6) {
+                fb[b % NB] = xfrag(ks, TO1 + 64);
+            } else if (k == 8) {
+                fb[b % NB] = xfrag(ks, TO8);
+            }
+        };
+        // step k: acc[k] = (tap T0 for k < 4, T1 for k < 8; co half k & 1, ci half (k >> 1) & 1), acc[8] = tap 8
+        auto mf = [&](int j) __attribute__((always_inline)) {
+            const int ks = j / 9, k = j - ks * 9, s = ks & 1, b = ks * 5 + k / 2;
+            if (k < 8) acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][k & 1], fb[b % NB], acc[k], 0, 0, 0);
+            else acc[8] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][C8], fb[b % NB], acc[8], 0, 0, 0);
+        };
+#pragma unroll
+        for (int j = 0; j < PD; ++j) rd(j);
+#pragma unroll
+        for (int j = 0; j < KS * 9; ++j) {
+            if (j + PD < KS * 9) rd(j + PD);
+            __builtin_amdgcn_sched_barrier(0);
+            mf(j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (ntile & 1) __syncthreads();  // the loaders' last (even-count) iteration
+    // slab[split][co][tap*ctot + cc*64 + ci]   (32x32 C layout: element i of lane l is row 8 (i / 4) + 4 (l / 32) + i % 4,
+    // column l % 32)
+    float* slab = p.slab + (size_t)split * p.M * p.N;
+    const int ctot = p.x.ctot;
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+        const int tap = a < 4 ? T0 : (a < 8 ? T1 : 8);
+        const int coh = a < 8 ? (a & 1) : C8, cih = a < 8 ? ((a >> 1) & 1) : I8;
+        const int ci = cc * 64 + cih * 32 + (lane & 31);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int co = mb + coh * 32 + 8 * (i / 4) + 4 * (lane >> 5) + i % 4;
+            slab[(size_t)co * p.N + tap * ctot + ci] = acc[a][i];
+        }
+    }
+}
+
+template <int HP, int DLD, int XLD, int DY_E, int BUF>
+__device__ __forceinline__ void ws_mfma32(const HWgArgs& p, const __bf16* smem, int lane, int wid, int cc, int mb,
+                                          int split, int ntile, int mvalid) {
+    constexpr int KS = WS_TPX / 16;
+    const int g = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
+    const int pk = 4 * (g >> 1) + q4, ch16 = 16 * (g & 1) + 4 * pp;
+    // byte offsets (within the halo region) of this lane's two halo pixels of each k-step at tap (0, 0)
+    unsigned xoff[KS][2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int m = ks * 16 + pk + 8 * h;
+            const int hm = m / p.tw;
+            const int px = m < mvalid ? hm * HP + (m - hm * p.tw) : 0;  // dy is 0 past the tile
+            xoff[ks][h] = (unsigned)(px * XLD + ch16) * 2u;
+        }
+    const unsigned aoff = (unsigned)(pk * DLD + ch16) * 2u;
+    switch (__builtin_amdgcn_readfirstlane(wid)) {
+    case 0: ws_mfma32_tiles<HP, DLD, XLD, DY_E, BUF, 0>(p, smem, lane, cc, mb, split, ntile, xoff, aoff); break;
+    case 1: ws_mfma32_tiles<HP, DLD, XLD, DY_E, BUF, 1>(p, smem, lane, cc, mb, split, ntile, xoff, aoff); break;
+    case 2: ws_mfma32_tiles<HP, DLD, XLD, DY_E, BUF, 2>(p, smem, lane, cc, mb, split, ntile, xoff, aoff); break;
+    default: ws_mfma32_tiles<HP, DLD, XLD, DY_E, BUF, 3>(p, smem, lane, cc, mb, split, ntile, xoff, aoff); break;
+    }
+}
+
+// MF32 (64 x 64 blocks only): the MFMA waves run v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (see the MF32 branch
+// of the MFMA waves); its fragments read 4 pixels x 32 channels per 32-lane group, so the rows are 96 elements
+// (48 dwords: 4 consecutive pixels fall on distinct 16-bank quarters)
+template <int COUT, int CIB, int HP, int HR, bool BNB, bool SPAN, bool MF32 = false>  // dy / x channels per block;
+                                                       // halo pitch and rows (tw+2 <= HP, th+2 <= HR); BNB:
+                                                       // BatchNorm-backward apply in the dy staging; SPAN: a block's x
+                                                       // channels may straddle the two sources of a concatenation
 __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_wgrad_ws(const HWgArgs p) {
     constexpr int KS = WS_TPX / 32;
     constexpr int NCI = CIB / 16, NCO = 4 / NCI, RM = COUT / 16 / NCO;  // wave grid and 16-row tiles per wave
     constexpr int DPP = COUT / 8, XPP = CIB / 8;                       // 16-B pieces per pixel (dy, x)
-    constexpr int DLD = COUT + 16, XLD = CIB + 16;                     // 96 / 160-B rows: conflict-free tr reads
+    constexpr int PAD = MF32 ? 32 : 16;
+    constexpr int DLD = COUT + PAD, XLD = CIB + PAD;                   // 96 / 160-B rows: conflict-free tr reads
     constexpr int DYP = WS_TPX * DPP / 256;                            // dy pieces per loader thread
     constexpr int HXP = (HP * HR * XPP + 255) / 256;                   // halo pieces per loader thread
     constexpr int DY_E = WS_TPX * DLD, BUF = DY_E + HXP * (256 / XPP) * XLD;  // elements per LDS buffer
     static_assert(RM >= 1 && NCI * NCO == 4, "wave grid");
+    static_assert(!MF32 || (COUT == 64 && CIB == 64 && !SPAN), "MF32: 64 x 64 blocks");
+    static_assert(2 * BUF * 2 <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2022,6 +2149,10 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
     }
 
     // =============================================================== MFMA waves
+    if constexpr (MF32) {
+        ws_mfma32<HP, DLD, XLD, DY_E, BUF>(p, smem, lane, wid, cc, mb, split, ntile, mvalid);
+        return;
+    }
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
     const int pc = 16 * (g >> 1) + 4 * (g & 1) + q;  // pixel within the k-step (0..23), +8 for the 2nd read
     const int ci0 = 16 * (wid % NCI), co0 = (wid / NCI) * (COUT / NCO);
@@ -2628,6 +2759,30 @@ static WsTile wgrad_tile_ws(int H, int W) {
     return best;
 }
 
+// SD_WS_MF32=1: the 64 x 64 blocks on v_mfma_f32_32x32x16_bf16 (opt-in, read per call). Bit-identical to the 16x16x32
+// form, and 4-9 % slower at every step shape (tools/conv_micro.py --wgrad-step, r06): DESIGN.md §3 r06
+static bool ws_mf32_enabled() {
+    const char* e = getenv("SD_WS_MF32");
+    return e && atoi(e) == 1;
+}
+
+// SD_WS_CO128 (read per call; 0 = off): the plain (no BatchNorm-backward) weight gradients with M % 128 == 0 take
+// 128 dy x 32 x channels per block instead of 64 x 64. The MFMA waves' layout is unchanged (each owns 64 dy rows x 16 x
+// channels x 9 taps, RM = 4) and so is the block count, hence the splits and the slab layout; per tile the loaders
+// transform and stage half the x halo (the BN+ReLU transform is their VALU, and the loaders paced the 64 x 64 blocks:
+// busy 92 % of their cycles at every step shape, tools/conv_micro.py SD_WG_DIAG) and LDS-DMA twice the dy rows (no VALU)
+static bool ws_co128_enabled() {
+    const char* e = getenv("SD_WS_CO128");
+    return !(e && atoi(e) == 0);
+}
+static WsCfg wgrad_ws_launch(int M, int N, int c0, bool bnb) {
+    WsCfg c = wgrad_ws(M, N, c0);
+    if (!bnb && c.cout == 64 && c.cib && !c.span && M % 128 == 0 && (N / 9) % 32 == 0 && c0 % 32 == 0 &&
+        ws_co128_enabled())
+        c = WsCfg{128, 32};
+    return c;
+}
+
 int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
     const WsCfg ws = wgrad_ws(M, N);
     HTile t = wgrad_tile(H, W);
@@ -2649,24 +2804,27 @@ int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
 
 const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W, bool bnb) {
     static thread_local char buf[64];
-    const WsCfg ws = wgrad_ws(M, N, c0);
+    const WsCfg ws = wgrad_ws_launch(M, N, c0, bnb);
     if (!ws.cib) return M == 32 ? (bnb ? "k_halo_wgrad<32, true>" : "k_halo_wgrad<32, false>") : "k_halo_wgrad<64, false>";
     const WsTile t = wgrad_tile_ws(H, W);
-    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s, %s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false",
-             ws.span ? "true" : "false");
+    const bool mf32 = ws.cout == 64 && ws.cib == 64 && ws_mf32_enabled();
+    snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s, %s%s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false",
+             ws.span ? "true" : "false", mf32 ? ", true" : "");
     return buf;
 }
 
-template <int COUT, int CIB, bool BNB, bool SPAN = false>
+template <int COUT, int CIB, bool BNB, bool SPAN = false, bool MF32 = false>
 static void launch_wgrad_ws(int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
     if (hp == 34)
-        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6, BNB, SPAN>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 34, 6, BNB, SPAN, MF32>), grid, dim3(512), 0, st, p);
     else
-        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8, BNB, SPAN>), grid, dim3(512), 0, st, p);
+        hipLaunchKernelGGL((k_halo_wgrad_ws<COUT, CIB, 22, 8, BNB, SPAN, MF32>), grid, dim3(512), 0, st, p);
 }
 template <bool BNB>
 static void launch_wgrad_ws(const WsCfg& ws, int hp, dim3 grid, hipStream_t st, const HWgArgs& p) {
-    if (ws.cout == 64 && ws.cib == 64) launch_wgrad_ws<64, 64, BNB>(hp, grid, st, p);
+    if (!BNB && ws.cout == 128) launch_wgrad_ws<128, 32, false>(hp, grid, st, p);
+    else if (ws.cout == 64 && ws.cib == 64 && ws_mf32_enabled()) launch_wgrad_ws<64, 64, BNB, false, true>(hp, grid, st, p);
+    else if (ws.cout == 64 && ws.cib == 64) launch_wgrad_ws<64, 64, BNB>(hp, grid, st, p);
     else if (ws.cout == 64) launch_wgrad_ws<64, 32, BNB>(hp, grid, st, p);
     else if (ws.cib == 64 && ws.span) launch_wgrad_ws<32, 64, BNB, true>(hp, grid, st, p);
     else if (ws.cib == 64) launch_wgrad_ws<32, 64, BNB>(hp, grid, st, p);
@@ -2685,7 +2843,7 @@ int sd_halo_wgrad_bnbwd_blocks(const sd_src& a, const sd_src& b, int M, int N) {
 
 int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int M, int N, float* slab, int splits,
                   hipStream_t st, const HaloBnBwd* bnb) {
-    const WsCfg ws = wgrad_ws(M, N, b.chans[0]);  // one source per block of x channels
+    const WsCfg ws = wgrad_ws_launch(M, N, b.chans[0], bnb != nullptr);  // one source per block of x channels
     const WsTile wt = wgrad_tile_ws(H, W);
     const HTile t = ws.cib ? HTile{wt.th, wt.tw, 4, 32} : wgrad_tile(H, W);
     HWgArgs p;

@@ -281,6 +281,104 @@ def test_conv3x3_wgrad_fused_bn_backward(B, H, W, ci, co):
     assert float((dw.cpu() - ref).abs().max()) <= 1e-2 * (1 + float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("B,H,W,c0,c1,co", [(2, 30, 40, 64, 0, 128), (1, 24, 64, 96, 0, 128), (1, 15, 20, 128, 0, 256),
+                                             (2, 17, 33, 64, 0, 128), (2, 20, 30, 32, 96, 128), (1, 30, 40, 128, 128, 256),
+                                             (1, 15, 20, 256, 256, 512)])
+def test_conv3x3_wgrad_co128_blocks_bit_identical(monkeypatch, B, H, W, c0, c1, co):
+    """Plain weight gradients with M % 128 == 0 run 128 dy x 32 x-channel blocks (default; SD_WS_CO128=0: 64 x 64).
+    Every MFMA wave keeps its 64 dy rows x 16 x channels x 9 taps and the split-K tile ranges are the same, so each dW
+    element is the same MFMA chain over the same pixels: the reduced dW are bit-identical. Single and concatenated
+    (dual-source, 32-aligned boundary) x, both halo layouts, ragged tiles; and against fp64."""
+    lib = L()
+    torch.manual_seed(13)
+    ys = [torch.randn(B, c, H, W).to(torch.bfloat16).float() for c in (c0, c1) if c]
+    bns = [((torch.rand(y.shape[1]) + 0.5) * torch.where(torch.rand(y.shape[1]) < 0.2, -1.0, 1.0),
+            torch.randn(y.shape[1]) * 0.3) for y in ys]
+    x = torch.cat([torch.relu(torch.addcmul(h.view(1, -1, 1, 1), y, s.view(1, -1, 1, 1))).to(torch.bfloat16).double()
+                   for y, (s, h) in zip(ys, bns)], 1)
+    ci = c0 + c1
+    dy = torch.randn(B, co, H, W).to(torch.bfloat16).float()
+    kw = dict(src1=_nhwc(ys[1], "bf16"), c1=c1, bn1=tuple(t.to(DEV) for t in bns[1])) if c1 else {}
+    b = lib.make_src(_nhwc(ys[0], "bf16"), c0, H, W, taps=9, bn0=tuple(t.to(DEV) for t in bns[0]), **kw)
+    a = lib.make_src(_nhwc(dy, "bf16"), co, H, W, taps=1)
+    sp = lib.call("sd_wgrad_splits", lib.SD_BF16, B, H, W, co, 9 * ci)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SD_WS_CO128", mode)
+        name = lib.kernel_name("sd_wgrad_kernel_name", lib.SD_BF16, a, b, co, 9 * ci)
+        assert name.startswith("k_halo_wgrad_ws<128, 32," if mode == "1" else "k_halo_wgrad_ws<64, "), name
+        slab = torch.empty(sp * co * 9 * ci, device=DEV)
+        dw = torch.empty(co, ci, 3, 3, device=DEV)
+        lib.call("sd_wgrad_gemm", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, slab.data_ptr(), sp, lib.stream_handle())
+        lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(),
+                 lib.stream_handle())
+        torch.cuda.synchronize()
+        out[mode] = dw.cpu()
+    assert torch.equal(out["1"], out["0"]), float((out["1"] - out["0"]).abs().max())
+    ref = torch.nn.grad.conv2d_weight(x, (co, ci, 3, 3), dy.double(), padding=1).float()
+    assert float((out["1"] - ref).abs().max()) <= 1e-3 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 30, 40, 64, 64), (1, 15, 20, 128, 128), (3, 17, 33, 64, 64),
+                                         (1, 24, 64, 64, 128), (2, 60, 80, 128, 64)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_conv3x3_wgrad_mfma32_matches_mfma16(monkeypatch, B, H, W, ci, co, fused):
+    """The 64 x 64-block weight gradient on v_mfma_f32_32x32x16_bf16 (SD_WS_MF32=1, opt-in) against its default
+    v_mfma_f32_16x16x32_bf16 form on the same bf16 operands: both accumulate the same 16-pixel chunks in the same order
+    (the 16x16x32 k-step's two k halves are pixels 0-15 and 16-31), so the reduced dW and the fused BatchNorm-backward
+    dy stores are bit-identical (measured at every step shape, tools/conv_micro.py --wgrad-step); both against fp64."""
+    lib = L()
+    monkeypatch.setenv("SD_WS_CO128", "0")  # the 64 x 64 blocks at M % 128 == 0 too
+    torch.manual_seed(11)
+    yx = torch.randn(B, ci, H, W).to(torch.bfloat16).float()
+    scx = (torch.rand(ci) + 0.5) * torch.where(torch.rand(ci) < 0.2, -1.0, 1.0)
+    shx = torch.randn(ci) * 0.3
+    x = torch.relu(yx * scx.view(1, -1, 1, 1) + shx.view(1, -1, 1, 1)).to(torch.bfloat16).double()
+    b = lib.make_src(_nhwc(yx, "bf16"), ci, H, W, taps=9, bn0=(scx.to(DEV), shx.to(DEV)))
+    sp = lib.call("sd_wgrad_splits", lib.SD_BF16, B, H, W, co, 9 * ci)
+    if fused:
+        y = (torch.randn(B, co, H, W) * 2 + 0.5).to(torch.bfloat16).float()
+        da = torch.randn(B, co, H, W).to(torch.bfloat16).float()
+        sc, sh = torch.rand(co) + 0.5, torch.randn(co) * 0.2
+        mean, invstd = torch.randn(co) * 0.5, torch.rand(co) + 0.5
+        coef = torch.stack([sc, torch.randn(co) * 0.1, torch.randn(co) * 0.1], 1).contiguous()
+        dev = [t.to(DEV).contiguous() for t in (sc, sh, mean, invstd, coef)]
+        dad, yd = _nhwc(da, "bf16"), _nhwc(y, "bf16")
+    else:
+        dy = torch.randn(B, co, H, W).to(torch.bfloat16).float()
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SD_WS_MF32", mode)
+        slab = torch.empty(sp * co * 9 * ci, device=DEV)
+        dw = torch.empty(co, ci, 3, 3, device=DEV)
+        if fused:
+            dyd = torch.full((B * H * W, co), float("nan"), dtype=torch.bfloat16, device=DEV)
+            a = lib.make_src(dyd, co, H, W, taps=1)
+            lib.call("sd_wgrad_gemm_bnbwd", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, dad.data_ptr(), yd.data_ptr(),
+                     *[t.data_ptr() for t in dev], slab.data_ptr(), sp, lib.stream_handle())
+        else:
+            dyd = _nhwc(dy, "bf16")
+            a = lib.make_src(dyd, co, H, W, taps=1)
+            lib.call("sd_wgrad_gemm", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, slab.data_ptr(), sp, lib.stream_handle())
+        name = lib.kernel_name("sd_wgrad_kernel_name", lib.SD_BF16, a, b, co, 9 * ci)
+        assert name.endswith(", true>") == (mode == "1"), name
+        lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(),
+                 lib.stream_handle())
+        torch.cuda.synchronize()
+        out[mode] = (dw.cpu(), dyd.cpu().clone())
+    dw1, dw0 = out["1"][0], out["0"][0]
+    if fused:
+        assert torch.equal(out["1"][1], out["0"][1])
+        dyr = _from_nhwc(out["1"][1].to(DEV), B, H, W, co).double()
+    else:
+        dyr = dy.double()
+    ref = torch.nn.grad.conv2d_weight(x, (co, ci, 3, 3), dyr, padding=1).float()
+    scale = float(ref.abs().max())
+    assert torch.equal(dw1, dw0), float((dw1 - dw0).abs().max()) / scale
+    # x here is relu(y*sc + sh) with a separate multiply and add, the kernel's one fma: a rare x differs by a bf16 ulp
+    assert float((dw1 - ref).abs().max()) <= 1e-3 * scale
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,h,w_,ci,co", [(2, 5, 7, 32, 16), (2, 12, 20, 64, 32), (1, 15, 20, 128, 64),
                                           # k_convt (forward): many 128-pixel tiles per block, ragged last tile,

@@ -101,7 +101,8 @@ WGRAD_LAYERS = [  # (H, W, dy channels M, x channels ci)
 WGRAD_STEP = [(60, 80, 128, 128), (30, 40, 256, 128), (30, 40, 256, 256), (15, 20, 512, 256), (15, 20, 512, 512),
               (30, 40, 256, 512), (30, 40, 256, 256), (60, 80, 128, 256), (60, 80, 128, 128), (120, 160, 64, 128),
               (120, 160, 64, 64)]
-WGRAD_MODES = {"mf1": {"SD_WS_MF32": "1"}, "mf0": {"SD_WS_MF32": "0"}}
+WGRAD_MODES = {"mf1": {"SD_WS_MF32": "1", "SD_WS_CO128": "0"}, "mf0": {"SD_WS_MF32": "0", "SD_WS_CO128": "0"},
+               "co1": {"SD_WS_CO128": "1"}, "co0": {"SD_WS_CO128": "0"}}
 
 
 def wgrad(B, s, dev, layers=WGRAD_LAYERS, modes=("default",), rounds=1):
@@ -130,7 +131,7 @@ def wgrad(B, s, dev, layers=WGRAD_LAYERS, modes=("default",), rounds=1):
             best, ref, line = {}, None, f"wgrad {H}x{W} M={M} ci={ci}:"
             for _ in range(rounds):
                 for mode in modes:
-                    for k in ("SD_WS_MF32",):
+                    for k in ("SD_WS_MF32", "SD_WS_CO128"):
                         os.environ.pop(k, None)
                     os.environ.update(WGRAD_MODES.get(mode, {}))
                     t = _time(gemm)
