@@ -467,7 +467,16 @@ def cpu_autocast_bound(held: dict, chunk: int = 8):
     dev_ac = (oac - o32).abs()
     dev16 = (held["d16"] - held["d32"]).abs()
     flat = int(dev16.flatten().argmax())
-    return {"pairs": int(x.shape[0]), "hip_bf16_max": round(float(dev16.max()), 5),
+
+    def tail(d):  # the worst pixel of 4.9 M is one draw: the tail's counts and high quantiles beside it
+        f = d.flatten().double()
+        q = torch.quantile(f[torch.randperm(f.numel(), generator=torch.Generator().manual_seed(0))[:1 << 24]],
+                           torch.tensor([0.999, 0.99999], dtype=torch.float64))
+        return {"px_over_0.5": int((f > 0.5).sum()), "px_over_1": int((f > 1.0).sum()), "px_over_2": int((f > 2.0).sum()),
+                "q999": round(float(q[0]), 5), "q99999": round(float(q[1]), 5)}
+
+    return {"pairs": int(x.shape[0]), "pixels": int(dev16.numel()), "hip_bf16_tail": tail(dev16),
+            "reference_autocast_tail": tail(dev_ac), "hip_bf16_max": round(float(dev16.max()), 5),
             "reference_autocast_max": round(float(dev_ac.max()), 5),
             "hip_bf16_mean": round(float(dev16.mean()), 6), "reference_autocast_mean": round(float(dev_ac.mean()), 6),
             "reference_autocast_at_hip_worst_pixel": round(float(dev_ac.flatten()[flat]), 5),
