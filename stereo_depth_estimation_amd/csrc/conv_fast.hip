@@ -174,6 +174,94 @@ struct FwdArgs {
     int xcd;  // 1: XCD-aware tile order (gridDim.x * gridDim.y % 8 == 0), see k_conv_fwd_bf16
 };
 
+// The forward epilogue of one BM x BN tile (accumulators in the MFMA 16x16 layout of 2x2 waves): STATS rows, then
+// the bf16 tile staged through `smem` (>= BM x (BN + 8) elements, free of other readers on entry) and written as whole
+// 16-B pieces. bcol[jj]: PIXSHUF's bias of this lane's column jj (the caller loads it: k_conv_fwd_ring from LDS, so no
+// global load here makes the compiler drain its LDS-DMA ring). Shared by k_conv_fwd_bf16 and k_conv_fwd_ring.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void fwd_epilogue(const FwdArgs& p, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                             const float (&bcol)[BN / WN / 16], __bf16* smem, int m0, int n0, int mt) {
+    constexpr int WTM = BM / WM, WTN = BN / WN, RM = WTM / 16, RN = WTN / 16;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    if (p.epi == SD_EPI_STATS) {
+        float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+#pragma unroll
+        for (int jj = 0; jj < RN; ++jj) {
+            float s = 0.f, ss = 0.f;
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + wm * WTM + i * 16 + crow + r;
+                    // statistics of the values as stored (bf16), like a BN reading the stored tensor
+                    const float v = m < p.M ? (float)(__bf16)acc[i][jj][r] : 0.f;
+                    s += v;
+                    ss += v * v;
+                }
+            s += __shfl_xor(s, 16);
+            ss += __shfl_xor(ss, 16);
+            s += __shfl_xor(s, 32);
+            ss += __shfl_xor(ss, 32);
+            if (lane < 16) {
+                const int col = wn * WTN + jj * 16 + lane;
+                red[(wm * BN + col) * 2] = s;
+                red[(wm * BN + col) * 2 + 1] = ss;
+            }
+        }
+        __syncthreads();
+        if (tid < BN && n0 + tid < p.N) {
+            float s = 0.f, ss = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) {
+                s += red[(w * BN + tid) * 2];
+                ss += red[(w * BN + tid) * 2 + 1];
+            }
+            reinterpret_cast<float2*>(p.stats)[(size_t)mt * p.N + n0 + tid] = make_float2(s, ss);
+        }
+    }
+    // Stage the bf16 tile (bias added for PIXSHUF) through LDS as [row][col], then write whole 16-B
+    // pieces: rows of the NHWC output, SPLIT halves, or the 2x2 sub-pixel scatter of a convT.
+    constexpr int OLD = BN + 8;
+    __syncthreads();  // the STATS reduction and the last k-tile are done with smem
+    __bf16* st = smem;
+    const int C4 = p.N >> 2;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int jj = 0; jj < RN; ++jj) {
+                const int nl = wn * WTN + jj * 16 + ccol;
+                float v = acc[i][jj][r];
+                if (p.epi == SD_EPI_PIXSHUF) v += bcol[jj];
+                st[(wm * WTM + i * 16 + crow + r) * OLD + nl] = (__bf16)v;
+            }
+    __syncthreads();
+    for (int item = tid; item < BM * (BN / 8); item += 256) {
+        const int ml = item / (BN / 8), s8 = item - ml * (BN / 8);
+        const int m = m0 + ml, n = n0 + s8 * 8;
+        if (m >= p.M || n >= p.N) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(st + ml * OLD + s8 * 8);
+        if (p.epi == SD_EPI_STORE || p.epi == SD_EPI_STATS) {
+            *reinterpret_cast<uint4*>(p.out0 + (size_t)m * p.N + n) = v;
+        } else if (p.epi == SD_EPI_SPLIT) {
+            if (n < p.n_split)
+                *reinterpret_cast<uint4*>(p.out0 + (size_t)m * p.n_split + n) = v;
+            else
+                *reinterpret_cast<uint4*>(p.out1 + (size_t)m * (p.N - p.n_split) + (n - p.n_split)) = v;
+        } else {  // SD_EPI_PIXSHUF: column n = t*C + o, t = 2*dy + dx of the 2x2 output pixel block
+            const int t = n / C4, o = n - t * C4;
+            const uint32_t tt = fdiv(m, p.fW);
+            const int w = m - tt * p.W;
+            const int b = fdiv(tt, p.fH), h = tt - b * p.H;
+            const size_t pix = ((size_t)b * 2 * p.H + 2 * h + (t >> 1)) * (2 * p.W) + 2 * w + (t & 1);
+            *reinterpret_cast<uint4*>(p.out0 + pix * C4 + o) = v;
+        }
+    }
+}
+
 // FA: one unpooled source tensor with 1 tap (on the grid) or 4 sub-pixel taps (at twice its resolution), K a whole
 // number of 64-wide tiles, 32-bit offsets: each row's base offset is computed once and a K tile adds the tap's
 // constant offset (the general gather's per-load tap test and 64-bit address math paced the ConvTranspose GEMMs)
@@ -316,85 +404,202 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
         __syncthreads();
     }
 
-    // ---------------------------------------------------------------- epilogue
-    const int ccol = lane & 15, crow = (lane >> 4) * 4;
-    if (p.epi == SD_EPI_STATS) {
-        float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+    static_assert(BM * (BN + 8) <= NBUF * (ABUF + BBUF), "epilogue staging fits");
+    float bcol[RN];
 #pragma unroll
-        for (int jj = 0; jj < RN; ++jj) {
-            float s = 0.f, ss = 0.f;
-#pragma unroll
-            for (int i = 0; i < RM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = m0 + wm * WTM + i * 16 + crow + r;
-                    // statistics of the values as stored (bf16), like a BN reading the stored tensor
-                    const float v = m < p.M ? (float)(__bf16)acc[i][jj][r] : 0.f;
-                    s += v;
-                    ss += v * v;
-                }
-            s += __shfl_xor(s, 16);
-            ss += __shfl_xor(ss, 16);
-            s += __shfl_xor(s, 32);
-            ss += __shfl_xor(ss, 32);
-            if (lane < 16) {
-                const int col = wn * WTN + jj * 16 + lane;
-                red[(wm * BN + col) * 2] = s;
-                red[(wm * BN + col) * 2 + 1] = ss;
-            }
-        }
-        __syncthreads();
-        if (tid < BN && n0 + tid < p.N) {
-            float s = 0.f, ss = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) {
-                s += red[(w * BN + tid) * 2];
-                ss += red[(w * BN + tid) * 2 + 1];
-            }
-            reinterpret_cast<float2*>(p.stats)[(size_t)mt * p.N + n0 + tid] = make_float2(s, ss);
-        }
+    for (int jj = 0; jj < RN; ++jj) {
+        const int nl = wn * WTN + jj * 16 + (lane & 15), C4 = p.N >> 2;
+        const int n = n0 + nl < p.N ? n0 + nl : 0;
+        bcol[jj] = p.epi == SD_EPI_PIXSHUF ? p.bias[n - (n / C4) * C4] : 0.f;
     }
-    // Stage the bf16 tile (bias added for PIXSHUF) through LDS as [row][col], then write whole 16-B
-    // pieces: rows of the NHWC output, SPLIT halves, or the 2x2 sub-pixel scatter of a convT.
-    constexpr int OLD = BN + 8;
-    static_assert(BM * OLD <= NBUF * (ABUF + BBUF), "epilogue staging fits");
-    __syncthreads();  // the STATS reduction and the last k-tile are done with smem
-    __bf16* st = smem;
-    const int C4 = p.N >> 2;
+    fwd_epilogue<BM, BN, WM, WN>(p, acc, bcol, smem, m0, n0, mt);
+}
+
+// =====================================================================================
+// k_conv_fwd_ring: the data gradients of the 15x20 / 30x40 ConvTranspose layers (up3 / up4: K = 512-1024 over 600-1200
+// tiles) as a persistent kernel with an LDS-DMA ring. k_conv_fwd_bf16 keeps one K tile per block in flight (its layers
+// ran at 1.7 TB/s with MFMA busy 0.15, PMC r06a). Here one 512-thread block per CU owns a fixed set of 128 x 128 tiles
+// (half the weight re-reads of 64 x 128); waves 4-7 stream the A / B tiles of every (tile, K tile) step global -> LDS
+// with buffer_load ... lds into a 4-stage ring, three steps ahead and across tile boundaries, while waves 0-3 run the
+// MFMAs and the epilogue. The MFMA order (K tiles ascending, two 16x16x32 k-steps each, the swz() fragments) is
+// k_conv_fwd_bf16's: bit-identical outputs. Measured (bench per-layer times, same box, three runs): up4 dgrad (K = 1024)
+// 43-44 vs 46-48 us, routed here; up3 dgrad (K = 512: 8 K tiles per tile, an epilogue every 8 steps) 46-47 vs 46, not; with the MFMA waves issuing the DMA themselves 69 / 69 us (8 pieces per step, each holding
+// its wave 60-185 cycles, outlasted the step's 32 MFMAs). Untransformed sources only: the up4 forward (BN+ReLU
+// source) measured slower with the transform on either side (MFMA waves, after the fragment read: 58 vs 52 us;
+// loader waves, in LDS one step ahead: 67 us).
+// =====================================================================================
+constexpr int RG_BM = 128, RG_BN = 128, RG_ST = 4;
+constexpr int RG_STAGE = RG_BM * (RG_BN + 8);  // elements per stage: A + B tiles, or the epilogue's staging tile
+static_assert(RG_STAGE >= (RG_BM + RG_BN) * FBK, "a stage holds the A and B tiles");
+constexpr int RG_C4MAX = 512;  // PIXSHUF: bias entries (N / 4)
+
+__global__ __launch_bounds__(512, 1) void k_conv_fwd_ring(const FwdArgs p, int lcpt, unsigned a_bytes) {
+    constexpr int BM = RG_BM, BN = RG_BN, WM = 2, WN = 2, WTM = BM / WM, WTN = BN / WN, RM = WTM / 16, RN = WTN / 16;
+    constexpr unsigned OOB = 0x80000000u;
+    __shared__ __attribute__((aligned(16))) __bf16 ring[RG_ST * RG_STAGE];
+    __shared__ float sbias[RG_C4MAX];
+    // waves 0-3 run the MFMAs and the epilogue, waves 4-7 issue the LDS-DMA (a piece costs its issuing wave 60-185
+    // cycles, MI355X_MICROARCH.md: issued by the MFMA waves, the 8 pieces per step outlasted the step's 32 MFMAs)
+    const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
+    const bool loader = threadIdx.x >= 256;
+    const int wm = wid / WN, wn = wid % WN;
+    const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM, T = ntm * ntn;
+    // tiles of this block: XCD x (= blockIdx % 8, the hardware's round-robin) owns the contiguous range [lo, hi) of the
+    // N-fastest tile order, and its blocks take every (grid / 8)-th tile of it: the N tiles that re-read one A tile and
+    // the whole weight matrix stay in one L2
+    const int xcd = blockIdx.x & 7, li = blockIdx.x >> 3, nb8 = gridDim.x >> 3;
+    const int lo = (int)((long long)xcd * T / 8), hi = (int)((long long)(xcd + 1) * T / 8);
+    const int ntile = hi - lo > li ? (hi - lo - li + nb8 - 1) / nb8 : 0;
+    if (p.epi == SD_EPI_PIXSHUF)
+        for (int c = threadIdx.x; c < (p.N >> 2); c += 512) sbias[c] = p.bias[c];
+    if (ntile == 0) return;  // block-uniform; no barrier has been passed
+    const int S = ntile * p.ktiles;
+    const int cmask = (1 << lcpt) - 1;
+    const bool taps4 = p.a.taps == 4;
+
+    // DMA geometry: wave-instruction g = 4 * wid + j fills LDS slots 64 g .. 64 g + 63 (16 B each, 8 per 64-element
+    // row) of the A tile and of the B tile; lane l's slot is row 8 g + l / 8, physical chunk l % 8, i.e. logical chunk
+    // (l % 8) ^ ((row / 2) % 8) (swz())
+    int rrow[4], clog[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = (4 * wid + j) * 8 + (lane >> 3);
+        rrow[j] = row;
+        clog[j] = (lane & 7) ^ ((row >> 1) & 7);
+    }
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.a.p0, (short)0, (int)a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsb =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.wp, (short)0, p.N * p.kpad * 2, 0x00020000);
+    const unsigned lds0 = (unsigned)(uintptr_t)ring + (unsigned)wid * 4096u;
+
+    // DMA cursor: the (tile, K tile) step the next issue() loads
+    int d_i = 0, d_kt = 0;
+    unsigned a_pb[4], b_off[4];  // per row: source pixel of tap 0 (OOB past M), weight row byte offset (OOB past N)
+    auto tile_of = [&](int i, int& mt, int& nt) {
+        const int lin = lo + li + i * nb8;
+        mt = lin / ntn;
+        nt = lin - mt * ntn;
+    };
+    auto issue = [&](int s) __attribute__((always_inline)) {
+        const bool live = s < S;
+        if (live && d_kt == 0) {
+            int mt, nt;
+            tile_of(d_i, mt, nt);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int m = mt * BM + rrow[j];
+                const uint32_t mm = m < p.M ? m : 0;
+                const uint32_t t = fdiv(mm, p.fW);
+                const uint32_t w = mm - t * p.W;  // t = b * H + h
+                a_pb[j] = m < p.M ? (taps4 ? 4 * t * p.W + 2 * w : t * p.W + w) : OOB;
+                const int n = nt * BN + rrow[j];
+                b_off[j] = n < p.N ? (unsigned)(n * p.kpad) * 2u : OOB;
+            }
+        }
+        const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)((s % RG_ST) * RG_STAGE * 2));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = d_kt * FKC + clog[j];
+            const int tap = q >> lcpt, cc = q & cmask;
+            const unsigned toff = taps4 ? (unsigned)((tap >> 1) * 2 * p.W + (tap & 1)) : 0u;
+            const unsigned off =
+                live && a_pb[j] != OOB ? ((a_pb[j] + toff) * (unsigned)p.a.c0 + (unsigned)cc * 8u) * 2u : OOB;
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(off), "s"(m0b + (unsigned)j * 1024u), "s"(rsa)
+                : "memory");
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned off =
+                live && b_off[j] != OOB ? b_off[j] + (unsigned)(d_kt * FBK + clog[j] * 8) * 2u : OOB;
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(off), "s"(m0b + (unsigned)(BM * FBK * 2) + (unsigned)j * 1024u), "s"(rsb)
+                : "memory");
+        }
+        if (live && ++d_kt == p.ktiles) {
+            d_kt = 0;
+            ++d_i;
+        }
+    };
+
+    if (loader) {
+        // the same step sequence and barriers as the MFMA waves: one per step, two more in each tile's epilogue
+#pragma unroll
+        for (int s = 0; s < RG_ST - 1; ++s) issue(s);
+        int kt = 0;
+        for (int s = 0; s < S; ++s) {
+            // step s's loads (this wave's) have landed when at most the two later steps' 16 are outstanding; the
+            // barrier makes every loader's visible and retires step s - 1's readers of the stage refilled next
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"((RG_ST - 2) * 8) : "memory");
+            __syncthreads();
+            issue(s + RG_ST - 1);
+            if (++kt == p.ktiles) {
+                kt = 0;
+                __syncthreads();  // fwd_epilogue: MFMA waves done with the stage
+                __syncthreads();  // fwd_epilogue: staging tile written
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (out-of-range) ring loads land before exit
+        return;
+    }
+    f32x4 acc[RM][RN];
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int jj = 0; jj < RN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int c_i = 0, c_kt = 0, mt, nt;
+    tile_of(0, mt, nt);
+    for (int s = 0; s < S; ++s) {
+        __syncthreads();
+        const __bf16* As = ring + (s % RG_ST) * RG_STAGE;
+        const __bf16* Bs = As + BM * FBK;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 af[RM], bf[RN];
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+                af[i] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + i * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+#pragma unroll
+            for (int jj = 0; jj < RN; ++jj)
+                bf[jj] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + jj * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int jj = 0; jj < RN; ++jj)
+                    acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[jj], acc[i][jj], 0, 0, 0);
+        }
+        if (++c_kt == p.ktiles) {
+            const int m0 = mt * BM, n0 = nt * BN;
+            float bcol[RN];
 #pragma unroll
             for (int jj = 0; jj < RN; ++jj) {
-                const int nl = wn * WTN + jj * 16 + ccol;
-                float v = acc[i][jj][r];
-                if (p.epi == SD_EPI_PIXSHUF) {
-                    const int n = n0 + nl < p.N ? n0 + nl : 0;
-                    v += p.bias[n - (n / C4) * C4];
-                }
-                st[(wm * WTM + i * 16 + crow + r) * OLD + nl] = (__bf16)v;
+                const int n = n0 + wn * WTN + jj * 16 + (lane & 15), C4 = p.N >> 2;
+                const int nc = n < p.N ? n : 0;
+                bcol[jj] = p.epi == SD_EPI_PIXSHUF ? sbias[nc - (nc / C4) * C4] : 0.f;
             }
-    __syncthreads();
-    for (int item = tid; item < BM * (BN / 8); item += 256) {
-        const int ml = item / (BN / 8), s8 = item - ml * (BN / 8);
-        const int m = m0 + ml, n = n0 + s8 * 8;
-        if (m >= p.M || n >= p.N) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(st + ml * OLD + s8 * 8);
-        if (p.epi == SD_EPI_STORE || p.epi == SD_EPI_STATS) {
-            *reinterpret_cast<uint4*>(p.out0 + (size_t)m * p.N + n) = v;
-        } else if (p.epi == SD_EPI_SPLIT) {
-            if (n < p.n_split)
-                *reinterpret_cast<uint4*>(p.out0 + (size_t)m * p.n_split + n) = v;
-            else
-                *reinterpret_cast<uint4*>(p.out1 + (size_t)m * (p.N - p.n_split) + (n - p.n_split)) = v;
-        } else {  // SD_EPI_PIXSHUF: column n = t*C + o, t = 2*dy + dx of the 2x2 output pixel block
-            const int t = n / C4, o = n - t * C4;
-            const uint32_t tt = fdiv(m, p.fW);
-            const int w = m - tt * p.W;
-            const int b = fdiv(tt, p.fH), h = tt - b * p.H;
-            const size_t pix = ((size_t)b * 2 * p.H + 2 * h + (t >> 1)) * (2 * p.W) + 2 * w + (t & 1);
-            *reinterpret_cast<uint4*>(p.out0 + pix * C4 + o) = v;
+            // the epilogue's first barrier retires this stage's readers; its staging tile is this stage, refilled
+            // only after the next step's barrier
+            fwd_epilogue<BM, BN, WM, WN>(p, acc, bcol, ring + (s % RG_ST) * RG_STAGE, m0, n0, mt);
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int jj = 0; jj < RN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+            c_kt = 0;
+            if (++c_i < ntile) tile_of(c_i, mt, nt);
         }
     }
 }
@@ -660,8 +865,29 @@ int sd_fast_fwd_rows(long long M, int N) { return cdiv(M, pick_fwd(M, N).bm); }
 
 static int fwd_nbuf();
 
-const char* sd_fast_fwd_name(const sd_src& a, long long M, int N) {
+// k_conv_fwd_ring's shapes (-1: not routed there): the untransformed FA sources the 64 x 128 tiles would run with
+// K >= 1024 (the up4 ConvTranspose dgrad), a power-of-two channel count, a STORE / SPLIT / PIXSHUF epilogue (the STATS row count stays the tiled kernel's) and at
+// least 256 of its 128 x 128 tiles (one per CU). SD_FWD_RING=0 keeps them on k_conv_fwd_bf16 (read per call: A/B runs).
+static int ring_mode(const sd_src& a, long long M, int N, int epi) {
+    const char* e = getenv("SD_FWD_RING");
+    if (e && *e && atoi(e) == 0) return -1;
+    const FCfg c = pick_fwd(M, N);
+    const int c0 = a.chans[0], taps = a.taps;
+    if (!(ffa_shape(a) && c.bm == 64 && c.bn == 128)) return -1;
+    if (epi != SD_EPI_STORE && epi != SD_EPI_SPLIT && epi != SD_EPI_PIXSHUF) return -1;
+    if (c0 < 8 || (c0 & (c0 - 1)) != 0 || (taps * c0) % FBK != 0) return -1;
+    if (taps * c0 < 16 * FBK) return -1;  // >= 16 K tiles per output tile: at 8 (up3 dgrad) its epilogues cost the gain
+    if (M * taps * c0 * 2 > 0x7fffffffLL || (long long)N * 2048 > 0x7fffffffLL) return -1;
+    if (a.xform[0] != SD_IDENT) return -1;
+    if (epi == SD_EPI_PIXSHUF && N / 4 > RG_C4MAX) return -1;
+    if (cdiv(M, RG_BM) * cdiv(N, RG_BN) < 256) return -1;
+    return 0;
+}
+
+const char* sd_fast_fwd_name(const sd_src& a, long long M, int N, int epi) {
     static thread_local char buf[96];
+    const int rm = ring_mode(a, M, N, epi);
+    if (rm >= 0) return "k_conv_fwd_ring";
     const FCfg c = pick_fwd(M, N);
     const bool fa = ffa_shape(a);
     const bool one = fa && c.bm == 64 && c.bn == 128 && fwd_nbuf() == 1;  // the single-buffered instance
@@ -742,6 +968,21 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
         return !(e && atoi(e) == 0);
     }();
     p.xcd = xcd_env && grid.y > 1 && (grid.x * grid.y) % 8 == 0;
+    const int rm = ring_mode(a, M, N, epi);
+    if (rm >= 0) {
+        static const int ncu = [] {
+            int d = 0, n = 0;
+            (void)hipGetDevice(&d);
+            (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+            return n >= 8 ? n : 8;
+        }();
+        int lcpt = 0;
+        while ((8 << lcpt) < a.chans[0]) ++lcpt;
+        const unsigned a_bytes = (unsigned)(M * a.taps * a.chans[0] * 2);
+        const dim3 rgrid(ncu & ~7);  // one block per CU (139 KB of LDS), a multiple of the 8 XCDs
+        hipLaunchKernelGGL(k_conv_fwd_ring, rgrid, dim3(512), 0, st, p, lcpt, a_bytes);
+        return sd_check_launch("sd_conv_gemm(bf16 ring)");
+    }
     const bool fa = ffa_shape(a) && p.a.kchunks % FKC == 0 && (long long)M * (a.taps == 4 ? 4 : 1) * a.chans[0] < (1LL << 31);
     if (fa) {
         if (c.bn == 32)

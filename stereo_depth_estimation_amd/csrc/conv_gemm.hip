@@ -268,7 +268,7 @@ int sd_validate_src(const sd_src* s, const char* what) { return validate_src(s, 
 
 // bf16 fast path (conv_fast.hip)
 int sd_fast_fwd_rows(long long M, int N);
-const char* sd_fast_fwd_name(const sd_src& a, long long M, int N);
+const char* sd_fast_fwd_name(const sd_src& a, long long M, int N, int epi);
 int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, int epi, void* out0,
                       void* out1, int n_split, const float* bias, float* stats, hipStream_t st);
 // bf16 halo-tiled path for small output-channel 3x3 convs (conv_halo.hip)
@@ -303,7 +303,7 @@ extern "C" const char* sd_conv_gemm_kernel_name(int dtype, const sd_src* a, int 
                                 a->xform[0] != SD_BNRELU && (a->chans[1] == 0 || a->xform[1] != SD_BNRELU));
     if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, N, epi)) return sd_convt_fwd_name(*a, N);
     if (dtype == SD_BF16 && a && sd_convt_dgrad_ok(*a, N, epi)) return sd_convt_dgrad_name(*a, N, false);
-    if (dtype == SD_BF16 && a && !a->pool) return sd_fast_fwd_name(*a, M, N);
+    if (dtype == SD_BF16 && a && !a->pool) return sd_fast_fwd_name(*a, M, N, epi);
     const Cfg c = pick_cfg(M, N);
     const int wm = c.bn == 32 ? 4 : 2, wn = c.bn == 32 ? 1 : 2;
     snprintf(buf, sizeof(buf), "k_igemm<%s, %d, %d, %d, %d>", dtype == SD_BF16 ? "__bf16" : "float", c.bm, c.bn, wm, wn);

@@ -435,6 +435,63 @@ def test_convT_fwd_dgrad_wgrad_bias(prec, B, h, w_, ci, co):
     assert torch.allclose(db.cpu(), bias.grad, atol=1e-3 * (1 + (B * 4 * h * w_) ** 0.5 / 100))
 
 
+@pytest.mark.parametrize("case,B,h,w_,ci,co", [
+    ("fwd", 64, 15, 20, 512, 256),   # up4 forward shape, identity source, K = 512: stays on the tiled kernel
+    ("fwd", 63, 15, 20, 1024, 256),  # K = 1024, PIXSHUF + bias, ragged M (18900 rows): the ring
+    ("fwd_bn", 64, 15, 20, 512, 256),  # BN+ReLU source: stays on the tiled kernel
+    ("dgrad", 64, 15, 20, 512, 256),  # up4 dgrad: 4 sub-pixel taps of 256 channels, K = 1024
+    ("dgrad", 64, 30, 40, 256, 128),  # up3 dgrad: K = 512 (8 K tiles), stays on the tiled kernel
+    ("dgrad", 8, 64, 64, 128, 256),   # 8 x 64 x 64 rows, K = 1024, N = 128: 256 tiles, one per block
+    ("dgrad", 2, 64, 64, 128, 512),   # K = 2048 over 64 tiles: stays on the tiled kernel (< 256 tiles)
+])
+def test_conv_fwd_ring_bit_identical_to_tiled(monkeypatch, case, B, h, w_, ci, co):
+    """k_conv_fwd_ring (persistent, LDS-DMA ring, 128 x 128 tiles) stores exactly what k_conv_fwd_bf16 stores: the
+    same MFMA order over the same fragments (model.py:67-73 ConvTranspose2d data gradient; the forward's PIXSHUF
+    epilogue through an identity source)."""
+    lib = L()
+    torch.manual_seed(21)
+    s = lib.stream_handle()
+    wt = (torch.randn(ci, co, 2, 2) / (2 * ci ** 0.5)).to(torch.bfloat16).float()
+    if case.startswith("fwd"):
+        xr = torch.randn(B, ci, h, w_).to(torch.bfloat16).float()
+        bn = case == "fwd_bn"
+        sc, sh = (torch.rand(ci) + 0.5, torch.randn(ci) * 0.3) if bn else (torch.ones(ci), torch.zeros(ci))
+        bias = torch.randn(co)
+        kp = ((ci + 63) // 64) * 64
+        wp = torch.empty(4 * co * kp, dtype=torch.bfloat16, device=DEV)
+        lib.call("sd_pack_convT_w", lib.SD_BF16, wt.contiguous().to(DEV).data_ptr(), ci, co, 0, kp, wp.data_ptr(), s)
+        keep = [_nhwc(xr, "bf16"), sc.to(DEV), sh.to(DEV), bias.to(DEV)]
+        src = lib.make_src(keep[0], ci, h, w_, taps=1, bn0=(keep[1], keep[2]) if bn else None)
+        N, epi, rows, bptr = 4 * co, lib.SD_EPI_PIXSHUF, B * 4 * h * w_, keep[3].data_ptr()
+        x = torch.relu(xr * sc[None, :, None, None] + sh[None, :, None, None]).to(torch.bfloat16).float() if bn else xr
+        ref = F.conv_transpose2d(x.to(DEV), wt.to(DEV), bias.to(DEV), stride=2).cpu()
+        shape = (B, 2 * h, 2 * w_, co)
+    else:
+        dy = torch.randn(B, co, 2 * h, 2 * w_).to(torch.bfloat16).float()
+        kp = ((4 * co + 63) // 64) * 64
+        wp = torch.empty(ci * kp, dtype=torch.bfloat16, device=DEV)
+        lib.call("sd_pack_convT_w", lib.SD_BF16, wt.contiguous().to(DEV).data_ptr(), ci, co, 1, kp, wp.data_ptr(), s)
+        keep = [_nhwc(dy, "bf16")]
+        src = lib.make_src(keep[0], co, 2 * h, 2 * w_, taps=4)
+        N, epi, rows, bptr = ci, lib.SD_EPI_STORE, B * h * w_, None
+        ref = F.conv2d(dy.to(DEV), wt.to(DEV), stride=2).cpu()  # ConvTranspose2d's data gradient
+        shape = (B, h, w_, ci)
+    outs = {}
+    ring = case != "fwd_bn" and (4 * co if case == "dgrad" else ci) >= 1024 and (B * h * w_ + 127) // 128 * (
+        (N + 127) // 128) >= 256
+    for mode, kname in (("0", "k_conv_fwd_bf16<64, 128"), ("1", "k_conv_fwd_ring" if ring else "k_conv_fwd_bf16<64")):
+        monkeypatch.setenv("SD_FWD_RING", mode)
+        assert lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, h, w_, N, epi).startswith(kname)
+        out = torch.full((rows, shape[3]), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lib.call("sd_conv_gemm", lib.SD_BF16, src, B, h, w_, wp.data_ptr(), N, kp, epi, out.data_ptr(), None, 0, bptr,
+                 None, s)
+        torch.cuda.synchronize()
+        outs[mode] = out
+    assert torch.equal(outs["1"], outs["0"])
+    got = outs["1"].float().cpu().reshape(shape).permute(0, 3, 1, 2)
+    assert float((got - ref).abs().max()) <= _tol(ref, "bf16")
+
+
 def test_pool_bwd_first_max_tie_break_and_skip_add():
     lib = L()
     B, H, W, C = 1, 4, 4, 8
