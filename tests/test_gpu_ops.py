@@ -562,7 +562,7 @@ def test_pack_weights_multi_equals_per_tensor_packs(prec):
     lib = L()
     s = lib.stream_handle()
     torch.manual_seed(5)
-    convs = [(32, 6, 8), (64, 32, 32), (128, 256, 256)]  # (co, ci, ci_pad)
+    convs = [(32, 6, 8), (64, 32, 32), (128, 256, 256), (512, 16, 16)]  # (co, ci, ci_pad)
     ups = [(64, 32), (512, 256)]  # (ci, co)
     ws3 = [torch.randn(co, ci, 3, 3, device=DEV) for co, ci, _ in convs]
     wsT = [torch.randn(ci, co, 2, 2, device=DEV) for ci, co in ups]
