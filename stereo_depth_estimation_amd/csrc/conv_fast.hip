@@ -276,7 +276,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
     static_assert(WM * WN == 4, "4 waves");
     static_assert(NBUF == 1 || NBUF == 2, "one or two LDS buffers");
     constexpr int ABUF = BM * FBK, BBUF = BN * FBK;
-    __shared__ __attribute__((aligned(16))) __bf16 smem[NBUF * (ABUF + BBUF)];
+    constexpr int SMEM = NBUF * (ABUF + BBUF) > BM * (BN + 8) ? NBUF * (ABUF + BBUF) : BM * (BN + 8);  // + staging
+    __shared__ __attribute__((aligned(16))) __bf16 smem[SMEM];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
@@ -404,7 +405,6 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
         __syncthreads();
     }
 
-    static_assert(BM * (BN + 8) <= NBUF * (ABUF + BBUF), "epilogue staging fits");
     float bcol[RN];
 #pragma unroll
     for (int jj = 0; jj < RN; ++jj) {
@@ -416,17 +416,18 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(const FwdArgs p) {
 }
 
 // =====================================================================================
-// k_conv_fwd_ring: the data gradients of the 15x20 / 30x40 ConvTranspose layers (up3 / up4: K = 512-1024 over 600-1200
-// tiles) as a persistent kernel with an LDS-DMA ring. k_conv_fwd_bf16 keeps one K tile per block in flight (its layers
+// k_conv_fwd_ring (opt-in): the data gradients of the 15x20 / 30x40 ConvTranspose layers (up3 / up4: K = 512-1024 over
+// 600-1200 tiles) as a persistent kernel with an LDS-DMA ring. k_conv_fwd_bf16 keeps one K tile per block in flight (its layers
 // ran at 1.7 TB/s with MFMA busy 0.15, PMC r06a). Here one 512-thread block per CU owns a fixed set of 128 x 128 tiles
 // (half the weight re-reads of 64 x 128); waves 4-7 stream the A / B tiles of every (tile, K tile) step global -> LDS
 // with buffer_load ... lds into a 4-stage ring, three steps ahead and across tile boundaries, while waves 0-3 run the
 // MFMAs and the epilogue. The MFMA order (K tiles ascending, two 16x16x32 k-steps each, the swz() fragments) is
-// k_conv_fwd_bf16's: bit-identical outputs. Measured (bench per-layer times, same box, three runs): up4 dgrad (K = 1024)
-// 43-44 vs 46-48 us, routed here; up3 dgrad (K = 512: 8 K tiles per tile, an epilogue every 8 steps) 46-47 vs 46, not; with the MFMA waves issuing the DMA themselves 69 / 69 us (8 pieces per step, each holding
-// its wave 60-185 cycles, outlasted the step's 32 MFMAs). Untransformed sources only: the up4 forward (BN+ReLU
-// source) measured slower with the transform on either side (MFMA waves, after the fragment read: 58 vs 52 us;
-// loader waves, in LDS one step ahead: 67 us).
+// k_conv_fwd_bf16's: bit-identical outputs. Measured (bench per-layer times, same box): up4 dgrad (K = 1024) 43-44 us
+// against 46-48 for 64 x 128 tiles but 41 for the single-buffered 128 x 128 ones (now the default there), up3 dgrad
+// (K = 512: an epilogue every 8 steps with no other block to overlap it) 46-47; with the MFMA waves issuing the DMA
+// themselves 69 / 69 us (8 pieces per step, each holding its wave 60-185 cycles, outlasted the step's 32 MFMAs). The
+// up4 forward (BN+ReLU source) measured slower with the transform on either side (MFMA waves, after the fragment
+// read: 58 vs 52 us; loader waves, in LDS one step ahead: 67 us). Opt-in: SD_FWD_RING=1 (ring_mode).
 // =====================================================================================
 constexpr int RG_BM = 128, RG_BN = 128, RG_ST = 4;
 constexpr int RG_STAGE = RG_BM * (RG_BN + 8);  // elements per stage: A + B tiles, or the epilogue's staging tile
@@ -830,16 +831,17 @@ __global__ __launch_bounds__(256) void k_bnrelu_pool_bf16(const __bf16* __restri
 struct FCfg {
     int bm, bn, wm, wn;
 };
-FCfg pick_fwd(long long M, int N) {
-    static const int bm_env = [] {  // SD_FWD_BM=128: 128-row tiles for N > 64 at large M (A/B runs)
-        const char* e = getenv("SD_FWD_BM");
-        return e ? atoi(e) : 0;
-    }();
+// fa1: the shape runs the single-buffered FA instances (k_conv_fwd_bf16<..., true, 1>)
+FCfg pick_fwd(long long M, int N, bool fa1) {
+    const char* e = getenv("SD_FWD_BM");  // 64 / 128: the row tile for N > 64 at large M (read per call: A/B, tests)
+    const int bm_env = e && *e ? atoi(e) : 0;
     if (N <= 32) return {256, 32, 4, 1};
     if (N <= 64) return {128, 64, 2, 2};
-    // 64-row tiles unless SD_FWD_BM=128: twice the blocks for the ConvTranspose dgrad / up4 GEMMs, whose blocks
-    // wait on one global round trip per K tile (measured: up4 dgrad 67 -> 54 us, up3 62 -> 57, up2 equal)
-    if (M >= 128LL * 96 && bm_env == 128) return {128, 128, 2, 2};
+    // 128 x 128 at large M in the single-buffered FA form: a third fewer bytes staged per MAC than 64 x 128, at three
+    // blocks per CU (the up3 / up4 ConvTranspose GEMMs, r06 gpurun_out/g10ab: up4 fwd 51 -> 44 us, up4 dgrad 46 ->
+    // 41, up3 dgrad 46 -> 40). The double-buffered 128-row tiles hold two blocks per CU and measured slower than
+    // 64 x 128 (r03: up4 dgrad 67 vs 54 us), so the general gather keeps 64 rows.
+    if (M >= 128LL * 96 && (bm_env == 128 || (bm_env != 64 && fa1))) return {128, 128, 2, 2};
     return {64, 128, 2, 2};
 }
 FCfg pick_wg(int M, int N) {
@@ -861,19 +863,25 @@ static bool ffa_shape(const sd_src& a) {
 }
 
 // ---------------------------------------------------------------------- host dispatch (bf16)
-int sd_fast_fwd_rows(long long M, int N) { return cdiv(M, pick_fwd(M, N).bm); }
-
 static int fwd_nbuf();
 
-// k_conv_fwd_ring's shapes (-1: not routed there): the untransformed FA sources the 64 x 128 tiles would run with
-// K >= 1024 (the up4 ConvTranspose dgrad), a power-of-two channel count, a STORE / SPLIT / PIXSHUF epilogue (the STATS row count stays the tiled kernel's) and at
-// least 256 of its 128 x 128 tiles (one per CU). SD_FWD_RING=0 keeps them on k_conv_fwd_bf16 (read per call: A/B runs).
+// the FA gather (one unpooled source, 1 or 4 taps, K a whole number of tiles, 32-bit element offsets)
+static bool fa_path(const sd_src& a, long long M) {
+    return ffa_shape(a) && M * (a.taps == 4 ? 4 : 1) * a.chans[0] < (1LL << 31);
+}
+
+// the STATS epilogue's row count (3x3 sources: never the FA gather)
+int sd_fast_fwd_rows(long long M, int N) { return cdiv(M, pick_fwd(M, N, false).bm); }
+
+// k_conv_fwd_ring's shapes, opt-in (SD_FWD_RING=1, read per call; -1: not routed there): untransformed FA sources with
+// N > 64 and K >= 1024 (the up4 ConvTranspose dgrad), a power-of-two channel count, a STORE / SPLIT / PIXSHUF epilogue
+// (the STATS row count stays the tiled kernel's) and at least 256 of its 128 x 128 tiles (one per CU). Measured slower
+// than the single-buffered 128 x 128 tiles (up4 dgrad 44 vs 41 us), faster than the 64 x 128 ones.
 static int ring_mode(const sd_src& a, long long M, int N, int epi) {
     const char* e = getenv("SD_FWD_RING");
-    if (e && *e && atoi(e) == 0) return -1;
-    const FCfg c = pick_fwd(M, N);
+    if (!(e && *e && atoi(e) == 1)) return -1;
     const int c0 = a.chans[0], taps = a.taps;
-    if (!(ffa_shape(a) && c.bm == 64 && c.bn == 128)) return -1;
+    if (!(fa_path(a, M) && N > 64)) return -1;
     if (epi != SD_EPI_STORE && epi != SD_EPI_SPLIT && epi != SD_EPI_PIXSHUF) return -1;
     if (c0 < 8 || (c0 & (c0 - 1)) != 0 || (taps * c0) % FBK != 0) return -1;
     if (taps * c0 < 16 * FBK) return -1;  // >= 16 K tiles per output tile: at 8 (up3 dgrad) its epilogues cost the gain
@@ -888,9 +896,9 @@ const char* sd_fast_fwd_name(const sd_src& a, long long M, int N, int epi) {
     static thread_local char buf[96];
     const int rm = ring_mode(a, M, N, epi);
     if (rm >= 0) return "k_conv_fwd_ring";
-    const FCfg c = pick_fwd(M, N);
-    const bool fa = ffa_shape(a);
-    const bool one = fa && c.bm == 64 && c.bn == 128 && fwd_nbuf() == 1;  // the single-buffered instance
+    const bool fa = fa_path(a, M);
+    const FCfg c = pick_fwd(M, N, fa && fwd_nbuf() == 1);
+    const bool one = fa && c.bn == 128 && fwd_nbuf() == 1;  // the single-buffered instances
     snprintf(buf, sizeof(buf), "k_conv_fwd_bf16<%d, %d, %d, %d, %s%s>", c.bm, c.bn, c.wm, c.wn, fa ? "true" : "false",
              one ? ", 1" : "");
     return buf;
@@ -961,7 +969,8 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
     p.n_split = n_split;
     p.bias = bias;
     p.stats = stats;
-    const FCfg c = pick_fwd(M, N);
+    const bool fa = fa_path(a, M);
+    const FCfg c = pick_fwd(M, N, fa && fwd_nbuf() == 1);
     dim3 grid(cdiv(M, c.bm), cdiv(N, c.bn));
     static const bool xcd_env = [] {
         const char* e = getenv("SD_FAST_XCD");
@@ -983,12 +992,13 @@ int sd_fast_conv_gemm(const sd_src& a, int batch, int H, int W, const void* wpac
         hipLaunchKernelGGL(k_conv_fwd_ring, rgrid, dim3(512), 0, st, p, lcpt, a_bytes);
         return sd_check_launch("sd_conv_gemm(bf16 ring)");
     }
-    const bool fa = ffa_shape(a) && p.a.kchunks % FKC == 0 && (long long)M * (a.taps == 4 ? 4 : 1) * a.chans[0] < (1LL << 31);
     if (fa) {
         if (c.bn == 32)
             hipLaunchKernelGGL((k_conv_fwd_bf16<256, 32, 4, 1, true>), grid, dim3(256), 0, st, p);
         else if (c.bn == 64)
             hipLaunchKernelGGL((k_conv_fwd_bf16<128, 64, 2, 2, true>), grid, dim3(256), 0, st, p);
+        else if (c.bm == 128 && fwd_nbuf() == 1)
+            hipLaunchKernelGGL((k_conv_fwd_bf16<128, 128, 2, 2, true, 1>), grid, dim3(256), 0, st, p);
         else if (c.bm == 128)
             hipLaunchKernelGGL((k_conv_fwd_bf16<128, 128, 2, 2, true>), grid, dim3(256), 0, st, p);
         else if (fwd_nbuf() == 1)

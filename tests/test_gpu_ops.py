@@ -444,10 +444,10 @@ def test_convT_fwd_dgrad_wgrad_bias(prec, B, h, w_, ci, co):
     ("dgrad", 8, 64, 64, 128, 256),   # 8 x 64 x 64 rows, K = 1024, N = 128: 256 tiles, one per block
     ("dgrad", 2, 64, 64, 128, 512),   # K = 2048 over 64 tiles: stays on the tiled kernel (< 256 tiles)
 ])
-def test_conv_fwd_ring_bit_identical_to_tiled(monkeypatch, case, B, h, w_, ci, co):
-    """k_conv_fwd_ring (persistent, LDS-DMA ring, 128 x 128 tiles) stores exactly what k_conv_fwd_bf16 stores: the
-    same MFMA order over the same fragments (model.py:67-73 ConvTranspose2d data gradient; the forward's PIXSHUF
-    epilogue through an identity source)."""
+def test_conv_fwd_tilings_bit_identical(monkeypatch, case, B, h, w_, ci, co):
+    """The FA GEMMs' three forms store the same bits: k_conv_fwd_bf16 at 64 x 128 (SD_FWD_BM=64) and at 128 x 128 (the
+    default at large M), and the opt-in k_conv_fwd_ring (persistent, LDS-DMA ring) — one MFMA order over the same
+    fragments (model.py:67-73: the ConvTranspose2d forward and its data gradient)."""
     lib = L()
     torch.manual_seed(21)
     s = lib.stream_handle()
@@ -477,18 +477,22 @@ def test_conv_fwd_ring_bit_identical_to_tiled(monkeypatch, case, B, h, w_, ci, c
         ref = F.conv2d(dy.to(DEV), wt.to(DEV), stride=2).cpu()  # ConvTranspose2d's data gradient
         shape = (B, h, w_, ci)
     outs = {}
-    ring = case != "fwd_bn" and (4 * co if case == "dgrad" else ci) >= 1024 and (B * h * w_ + 127) // 128 * (
-        (N + 127) // 128) >= 256
-    for mode, kname in (("0", "k_conv_fwd_bf16<64, 128"), ("1", "k_conv_fwd_ring" if ring else "k_conv_fwd_bf16<64")):
-        monkeypatch.setenv("SD_FWD_RING", mode)
-        assert lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, h, w_, N, epi).startswith(kname)
+    M = B * h * w_
+    ring = case != "fwd_bn" and (4 * co if case == "dgrad" else ci) >= 1024 and (M + 127) // 128 * ((N + 127) // 128) >= 256
+    big = "k_conv_fwd_bf16<128, 128, 2, 2, true, 1>" if M >= 128 * 96 else "k_conv_fwd_bf16<64, 128, 2, 2, true, 1>"
+    modes = (("64", "0", "k_conv_fwd_bf16<64, 128, 2, 2, true, 1>"), ("", "0", big),
+             ("", "1", "k_conv_fwd_ring" if ring else big))
+    for bm, rg, kname in modes:
+        monkeypatch.setenv("SD_FWD_BM", bm)
+        monkeypatch.setenv("SD_FWD_RING", rg)
+        assert lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, h, w_, N, epi) == kname
         out = torch.full((rows, shape[3]), float("nan"), dtype=torch.bfloat16, device=DEV)
         lib.call("sd_conv_gemm", lib.SD_BF16, src, B, h, w_, wp.data_ptr(), N, kp, epi, out.data_ptr(), None, 0, bptr,
                  None, s)
         torch.cuda.synchronize()
-        outs[mode] = out
-    assert torch.equal(outs["1"], outs["0"])
-    got = outs["1"].float().cpu().reshape(shape).permute(0, 3, 1, 2)
+        outs[bm + rg] = out
+    assert torch.equal(outs["0"], outs["640"]) and torch.equal(outs["1"], outs["640"])
+    got = outs["0"].float().cpu().reshape(shape).permute(0, 3, 1, 2)
     assert float((got - ref).abs().max()) <= _tol(ref, "bf16")
 
 
