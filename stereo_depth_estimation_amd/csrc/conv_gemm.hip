@@ -285,7 +285,7 @@ long long sd_halo_split_ws_bytes(const sd_src& a, int batch, int H, int W, int N
 int sd_halo_store_rows(int batch, int H, int W, int N, int ctot);
 bool sd_halo_bnsum_ok(const sd_src& a, int N);
 
-bool sd_convt_fwd_ok(const sd_src& a, int N, int epi);
+bool sd_convt_fwd_ok(const sd_src& a, long long M, int N, int epi);
 const char* sd_convt_fwd_name(const sd_src& a, int N);
 int sd_convt_fwd(const sd_src& a, int batch, int H, int W, const void* wpack, int N, int kpad, const float* bias,
                  void* out, hipStream_t st);
@@ -301,7 +301,7 @@ extern "C" const char* sd_conv_gemm_kernel_name(int dtype, const sd_src* a, int 
     if (dtype == SD_BF16 && a && sd_halo_fwd_ok(*a, N, epi))
         return sd_halo_fwd_name(H, W, N, epi, a->chans[0], a->chans[1], false, false, false,
                                 a->xform[0] != SD_BNRELU && (a->chans[1] == 0 || a->xform[1] != SD_BNRELU));
-    if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, N, epi)) return sd_convt_fwd_name(*a, N);
+    if (dtype == SD_BF16 && a && sd_convt_fwd_ok(*a, (long long)batch * H * W, N, epi)) return sd_convt_fwd_name(*a, N);
     if (dtype == SD_BF16 && a && sd_convt_dgrad_ok(*a, N, epi)) return sd_convt_dgrad_name(*a, N, false);
     if (dtype == SD_BF16 && a && !a->pool) return sd_fast_fwd_name(*a, M, N, epi);
     const Cfg c = pick_cfg(M, N);
@@ -354,7 +354,7 @@ extern "C" int sd_conv_gemm(int dtype, const sd_src* a, int batch, int H, int W,
         SD_REQUIRE(sd_halo_fwd_ok(*a, N, epi), "sd_conv_gemm: bf16 STATS with N=%d needs a 3x3 unpooled source", N);
     if (dtype == SD_BF16 && sd_halo_fwd_ok(*a, N, epi))
         return sd_halo_conv_fwd(*a, batch, H, W, wpack, N, kpad, epi, out0, out1, n_split, stats, to_stream(s));
-    if (dtype == SD_BF16 && sd_convt_fwd_ok(*a, N, epi))
+    if (dtype == SD_BF16 && sd_convt_fwd_ok(*a, (long long)batch * H * W, N, epi))
         return sd_convt_fwd(*a, batch, H, W, wpack, N, kpad, bias, out0, to_stream(s));
     if (dtype == SD_BF16 && sd_convt_dgrad_ok(*a, N, epi))
         return sd_convt_dgrad(*a, batch, H, W, wpack, N, kpad, out0, nullptr, nullptr, to_stream(s));

@@ -372,13 +372,17 @@ int ct_gper(int nblk, int NB, int K, long long M) {
 
 }  // namespace
 
-// bf16 ConvTranspose2d forward through k_convt: one unpooled 1-tap source, K % 64 == 0 and K <= SD_CONVT_KMAX
-// (default 256), N = 4*C with C % 32 == 0 and N % 64 == 0 (up1..up3; up4's K = 512 slice holds one block per
-// CU, and the tiled GEMM measured faster there: 79 vs 115 us at B=64)
-bool sd_convt_fwd_ok(const sd_src& a, int N, int epi) {
-    static const int kmax = env_int("SD_CONVT_KMAX", 256);
+// bf16 ConvTranspose2d forward through k_convt: one unpooled 1-tap source, K % 64 == 0, N = 4*C with C % 32 == 0 and
+// N % 64 == 0, and K <= 128, or K <= SD_CONVT_KMAX (default 256, read per call) at M >= 16384 GEMM rows. up4's
+// K = 512 slice holds one block per CU, and the tiled GEMM measured faster there (79 vs 115 us at B=64). up3 (K = 256):
+// at B = 64 (M = 76800) k_convt and the tiled GEMM's 128 x 128 tiles measured even over the step (per layer 64 vs 55
+// us, bench 7708 vs 7681 mean of three, gpurun_out/g14ab-g16ab); at the live app's B = 1 (M = 10800) the tiled GEMM
+// took the fp8 forward 0.587-0.593 -> 0.579 ms (gpurun_out/g15)
+bool sd_convt_fwd_ok(const sd_src& a, long long M, int N, int epi) {
+    const int kmax = env_int("SD_CONVT_KMAX", 256);
     const int K = a.chans[0] + a.chans[1];
-    return epi == SD_EPI_PIXSHUF && a.taps == 1 && !a.pool && a.chans[1] == 0 && K % CT_KC == 0 && K <= kmax &&
+    return epi == SD_EPI_PIXSHUF && a.taps == 1 && !a.pool && a.chans[1] == 0 && K % CT_KC == 0 &&
+           (K <= 128 || (K <= kmax && M >= 16384)) &&
            K <= CT_KMAX_BN && (N / 4) % 32 == 0 && pick_nb(N, K) != 0 &&
            (a.xform[0] == SD_IDENT || a.xform[0] == SD_BNRELU);
 }

@@ -381,8 +381,8 @@ def test_conv3x3_wgrad_mfma32_matches_mfma16(monkeypatch, B, H, W, ci, co, fused
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,h,w_,ci,co", [(2, 5, 7, 32, 16), (2, 12, 20, 64, 32), (1, 15, 20, 128, 64),
-                                          # k_convt (forward): many 128-pixel tiles per block, ragged last tile,
-                                          # K 256 / 512 (weights slice of 66 / 133 KB in LDS)
+                                          # k_convt (forward, K <= 128): many 128-pixel tiles per block, ragged
+                                          # last tile; K 256 / 512: the tiled GEMM
                                           (3, 60, 90, 64, 32), (2, 9, 13, 256, 128), (1, 6, 10, 512, 256)])
 def test_convT_fwd_dgrad_wgrad_bias(prec, B, h, w_, ci, co):
     lib = L()
@@ -686,6 +686,34 @@ def test_heads_bnsum_matches_heads_then_reduce(prec, C, P):
     assert float((d > 2 ** -7 * da2.float().abs()).float().mean()) == 0.0
     assert torch.allclose(p1, p2, rtol=1e-5, atol=1e-5)
     assert torch.allclose(bn1, bn2, rtol=1e-4, atol=1e-4 * (1 + float(bn2.abs().max())))
+
+
+@pytest.mark.parametrize("kmax,kname", [("256", "k_convt<1, "), ("128", "k_conv_fwd_bf16<")])
+def test_convT_fwd_k256_both_routes(monkeypatch, kmax, kname):
+    """The up3-shaped ConvTranspose2d forward (K = 256, BN+ReLU source, M = 19200 GEMM rows) through k_convt (the weight
+    slice in LDS; the default at M >= 16384) and through the tiled GEMM (SD_CONVT_KMAX=128; the default below that M),
+    both against the fp32 reference."""
+    lib = L()
+    monkeypatch.setenv("SD_CONVT_KMAX", kmax)
+    torch.manual_seed(12)
+    B, h, w_, ci, co = 16, 30, 40, 256, 128
+    xr = torch.randn(B, ci, h, w_).to(torch.bfloat16).float()
+    sc, sh = torch.rand(ci) + 0.5, torch.randn(ci) * 0.3
+    x = torch.relu(xr * sc[None, :, None, None] + sh[None, :, None, None]).to(torch.bfloat16).float()
+    wt = (torch.randn(ci, co, 2, 2) / 16).to(torch.bfloat16).float()
+    bias = torch.randn(co)
+    ref = F.conv_transpose2d(x.to(DEV), wt.to(DEV), bias.to(DEV), stride=2).cpu()
+    s = lib.stream_handle()
+    wpf = torch.empty(4 * co * ci, dtype=torch.bfloat16, device=DEV)
+    lib.call("sd_pack_convT_w", lib.SD_BF16, wt.contiguous().to(DEV).data_ptr(), ci, co, 0, ci, wpf.data_ptr(), s)
+    keep = [_nhwc(xr, "bf16"), sc.to(DEV), sh.to(DEV), bias.to(DEV)]
+    src = lib.make_src(keep[0], ci, h, w_, taps=1, bn0=(keep[1], keep[2]))
+    assert lib.kernel_name("sd_conv_gemm_kernel_name", lib.SD_BF16, src, B, h, w_, 4 * co,
+                           lib.SD_EPI_PIXSHUF).startswith(kname)
+    out = torch.empty(B * 4 * h * w_, co, dtype=torch.bfloat16, device=DEV)
+    lib.call("sd_conv_gemm", lib.SD_BF16, src, B, h, w_, wpf.data_ptr(), 4 * co, ci, lib.SD_EPI_PIXSHUF,
+             out.data_ptr(), None, 0, keep[3].data_ptr(), None, s)
+    assert float((_from_nhwc(out, B, 2 * h, 2 * w_, co) - ref).abs().max()) <= _tol(ref, "bf16")
 
 
 def test_convT_fwd_identity_source():
