@@ -1449,7 +1449,12 @@ constexpr int WG_MAXPX = 256;   // pixels per wgrad tile (8 k-steps)
 
 
 
-template <int COUT, bool BNB>  // BNB: BatchNorm-backward apply in the dy staging (no dy written: enc1.0 has no dgrad)
+// BNB: BatchNorm-backward apply in the dy staging (no dy written: enc1.0 has no dgrad). X8: an x source of at most 8
+// channels (enc1.0's padded input): one 8-channel piece per halo pixel, 2 per thread instead of 6 pieces of which 3 in 4
+// were past the channels (loaded from a clamped address and discarded). The chunk's other pieces are never written:
+// they only feed the dW columns of channels >= 8, which the slab write skips. The freed registers hold a second tile
+// in flight (BNB, one (da, y) set: latency-bound at 3.9 TB/s, r06).
+template <int COUT, bool BNB, bool X8 = false>
 __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // two blocks per CU (LDS: 63-80 KB)
     constexpr int DY_LD = COUT + 16;             // 96 B / 160 B rows: conflict-free transposed reads
     constexpr int RM = COUT / 32;                // 16-row tiles of output channels per wave
@@ -1505,10 +1510,11 @@ __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // tw
             kbn[3 * COUT + j] = is * k2 * sh + sc * (p.bmu[c] * is * k2 - k1);
         }
     }
-    int hgeo[HP_PER_THREAD];                     // (row << 16 | col) of this thread's halo pieces
+    constexpr int HPT = X8 ? (HMAX + 255) / 256 : HP_PER_THREAD;  // halo pieces per thread
+    int hgeo[HPT];                               // (row << 16 | col) of this thread's halo pieces
 #pragma unroll
-    for (int i = 0; i < HP_PER_THREAD; ++i) {
-        const int px = wg_pixel(tid + i * 256);
+    for (int i = 0; i < HPT; ++i) {
+        const int px = X8 ? tid + i * 256 : wg_pixel(tid + i * 256);
         const int hy = px / p.hw;
         hgeo[i] = px < p.nhalo ? (hy << 16 | (px - hy * p.hw)) : -1;
     }
@@ -1524,11 +1530,12 @@ __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // tw
     // two for M = 32 (one tile of cover was shorter than an HBM round trip at full resolution; three
     // measured no faster)
     // (BNB: one, the raw (da, y) pair of a second set does not fit beside the halo in two waves per SIMD)
-    constexpr int WS = COUT == 32 && !BNB ? 2 : 1;
-    uint4 dr[WS][DY_PER_THREAD], xr[WS][HP_PER_THREAD];
+    constexpr int WS = COUT == 32 && (!BNB || X8) ? 2 : 1;
+    uint4 dr[WS][DY_PER_THREAD], xr[WS][HPT];
     uint4 yr[BNB ? WS : 1][BNB ? DY_PER_THREAD : 1];  // BNB: the raw y pieces beside da in dr
     unsigned dmask[WS], xmask[WS];  // bit i: piece i valid (else stored as zeros)
-    const HaloCol hc = halo_col(p.x, cc * CK + wg_piece(tid) * 8, p.slab);  // fixed for the whole block (slab: any valid address)
+    // fixed for the whole block (slab: any valid address)
+    const HaloCol hc = halo_col(p.x, cc * CK + (X8 ? 0 : wg_piece(tid)) * 8, p.slab);
     auto load_tile = [&](auto S, int tile) __attribute__((always_inline)) {
         const int tx = tile % p.tiles_x;
         const int rest = tile / p.tiles_x;
@@ -1548,7 +1555,7 @@ __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // tw
             if constexpr (BNB) yr[S][i] = *reinterpret_cast<const uint4*>(p.by + off);
         }
 #pragma unroll
-        for (int i = 0; i < HP_PER_THREAD; ++i) {
+        for (int i = 0; i < HPT; ++i) {
             const int g = hgeo[i];
             const int h = h0 - 1 + (g >> 16), w = w0 - 1 + (g & 0xffff);
             const bool ok = (g >= 0) & hc.cok & (h >= 0) & (w >= 0) & (h < p.H) & (w < p.W);
@@ -1579,10 +1586,15 @@ __global__ __launch_bounds__(256, 2) void k_halo_wgrad(const HWgArgs p) {  // tw
             *reinterpret_cast<uint4*>(dys + m * DY_LD + s * 8) = ((dmask[S] >> i) & 1u) ? v : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < HP_PER_THREAD; ++i) {  // every piece lands inside the HMAX-pixel region
+        for (int i = 0; i < HPT; ++i) {  // every piece lands inside the HMAX-pixel region
             const int item = tid + i * 256;
-            *reinterpret_cast<uint4*>(hxs + wg_pixel(item) * XW_LD + wg_piece(item) * 8) =
-                halo_finish_pk(hc, (xmask[S] >> i) & 1u, xr[S][i]);
+            if constexpr (X8) {
+                if (item < HMAX)
+                    *reinterpret_cast<uint4*>(hxs + item * XW_LD) = halo_finish_pk(hc, (xmask[S] >> i) & 1u, xr[S][i]);
+            } else {
+                *reinterpret_cast<uint4*>(hxs + wg_pixel(item) * XW_LD + wg_piece(item) * 8) =
+                    halo_finish_pk(hc, (xmask[S] >> i) & 1u, xr[S][i]);
+            }
         }
     };
     constexpr std::integral_constant<int, 0> S0{};
@@ -2276,6 +2288,14 @@ static bool halo_xcd_enabled() {
     return on;
 }
 
+// k_halo_wgrad's 8-channel x layout (X8) for sources of at most 8 channels (SD_WG_X8=0: the 32-channel chunk layout,
+// read per call: A/B runs, tests)
+static bool wg_x8(int ctot) {
+    const char* e = getenv("SD_WG_X8");
+    if (e && *e && atoi(e) == 0) return false;
+    return ctot > 0 && ctot <= 8;
+}
+
 // the all-LDS-DMA loaders for launches whose sources are all raw (SD_HALO_RAW=0: register-staged halos, A/B runs)
 static bool halo_raw_enabled() {  // read per call (A/B modes within one process)
     const char* e = getenv("SD_HALO_RAW");
@@ -2805,7 +2825,10 @@ int sd_halo_wgrad_splits(int batch, int H, int W, int M, int N) {
 const char* sd_halo_wgrad_name(int M, int N, int c0, int H, int W, bool bnb) {
     static thread_local char buf[64];
     const WsCfg ws = wgrad_ws_launch(M, N, c0, bnb);
-    if (!ws.cib) return M == 32 ? (bnb ? "k_halo_wgrad<32, true>" : "k_halo_wgrad<32, false>") : "k_halo_wgrad<64, false>";
+    if (!ws.cib)
+        return M == 32 ? (bnb ? (wg_x8(c0) ? "k_halo_wgrad<32, true, true>" : "k_halo_wgrad<32, true>")
+                              : "k_halo_wgrad<32, false>")
+                       : "k_halo_wgrad<64, false>";
     const WsTile t = wgrad_tile_ws(H, W);
     const bool mf32 = ws.cout == 64 && ws.cib == 64 && ws_mf32_enabled();
     snprintf(buf, sizeof(buf), "k_halo_wgrad_ws<%d, %d, %d, %d, %s, %s%s>", ws.cout, ws.cib, t.hp, t.hr, bnb ? "true" : "false",
@@ -2893,7 +2916,10 @@ int sd_halo_wgrad(const sd_src& a, const sd_src& b, int batch, int H, int W, int
             sd_set_error("sd_wgrad_gemm_bnbwd: k_halo_wgrad fuses M = 32 without a dy destination only (M=%d)", M);
             return SD_EINVAL;
         }
-        hipLaunchKernelGGL((k_halo_wgrad<32, true>), dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
+        if (wg_x8(p.x.ctot))
+            hipLaunchKernelGGL((k_halo_wgrad<32, true, true>), dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
+        else
+            hipLaunchKernelGGL((k_halo_wgrad<32, true>), dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
     } else if (M == 32) {
         hipLaunchKernelGGL((k_halo_wgrad<32, false>), dim3(cdiv(p.x.ctot, CK), splits, 1), dim3(256), 0, st, p);
     } else {

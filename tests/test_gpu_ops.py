@@ -231,11 +231,12 @@ def test_conv3x3_wgrad_bn_relu_source(B, H, W, ci, co):
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 30, 40, 128, 64), (1, 15, 20, 128, 128), (2, 10, 14, 32, 64),
                                          (1, 24, 64, 32, 32), (1, 16, 64, 64, 32), (3, 17, 33, 64, 64),
                                          (1, 48, 64, 32, 32), (2, 15, 20, 256, 64),
-                                         # enc1.0: 8-channel x, no dgrad (dy not written; k_halo_wgrad<32, true>)
-                                         (2, 32, 64, 8, 32), (1, 30, 50, 8, 32)])
-def test_conv3x3_wgrad_fused_bn_backward(B, H, W, ci, co):
+                                         # enc1.0: 8-channel x, no dgrad (dy not written; k_halo_wgrad<32, true, true>)
+                                         (2, 32, 64, 8, 32), (1, 30, 50, 8, 32), (3, 70, 90, 8, 32)])
+def test_conv3x3_wgrad_fused_bn_backward(monkeypatch, B, H, W, ci, co):
     """sd_wgrad_gemm_bnbwd: dy = BatchNorm-backward apply of (da, y) formed while staging (written out for the
-    dgrad) and the weight gradient on it, vs sd_bn_bwd_apply's formula in fp32 then F.conv2d backward."""
+    dgrad) and the weight gradient on it, vs sd_bn_bwd_apply's formula in fp32 then F.conv2d backward. The 8-channel
+    x layout (two tiles in flight) writes the same slab bits as the 32-channel chunk layout (SD_WG_X8=0)."""
     lib = L()
     torch.manual_seed(5)
     yx = torch.randn(B, ci, H, W).to(torch.bfloat16).float()
@@ -270,6 +271,15 @@ def test_conv3x3_wgrad_fused_bn_backward(B, H, W, ci, co):
     dad, yd = _nhwc(da, "bf16"), _nhwc(y, "bf16")
     lib.call("sd_wgrad_gemm_bnbwd", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, dad.data_ptr(), yd.data_ptr(),
              *[t.data_ptr() for t in dev], slab.data_ptr(), sp, lib.stream_handle())
+    if ci <= 8:
+        assert lib.kernel_name("sd_wgrad_bnbwd_kernel_name", a, b, co, 9 * ci) == "k_halo_wgrad<32, true, true>"
+        monkeypatch.setenv("SD_WG_X8", "0")
+        slab0 = torch.empty_like(slab)
+        lib.call("sd_wgrad_gemm_bnbwd", lib.SD_BF16, a, b, B, H, W, co, 9 * ci, dad.data_ptr(), yd.data_ptr(),
+                 *[t.data_ptr() for t in dev], slab0.data_ptr(), sp, lib.stream_handle())
+        monkeypatch.delenv("SD_WG_X8")
+        torch.cuda.synchronize()
+        assert torch.equal(slab, slab0)
     lib.call("sd_wgrad_reduce", slab.data_ptr(), sp, co, 9 * ci, lib.SD_W_CONV3, ci, dw.data_ptr(), lib.stream_handle())
     got_dy = _from_nhwc(dyd, B, H, W, co)
     if write_dy:  # every dy element written once (no NaN left), each within bf16 rounding of the fp32 formula
