@@ -98,7 +98,7 @@ def test_planning_queries_are_host_only():
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, dy, x8, 32, 72) == 0  # enc1.0: only without a dy destination
     nody = L.make_src(None, 32, 240, 320, taps=1)
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_BF16, nody, x8, 32, 72) == 1
-    assert L.kernel_name("sd_wgrad_bnbwd_kernel_name", nody, x8, 32, 72) == "k_halo_wgrad<32, true>"
+    assert L.kernel_name("sd_wgrad_bnbwd_kernel_name", nody, x8, 32, 72) == "k_halo_wgrad<32, true, true>"  # the 8-channel x layout
     assert L.call("sd_wgrad_bnbwd_ok", L.SD_F32, dy, src, 32, 288) == 0
     # fp8 inference convs (live app, 960x720): one min/max row per persistent block
     assert L.call("sd_conv3x3_fp8_rows", 1, 720, 960, 32) == 256
