@@ -1887,7 +1887,10 @@ __global__ __launch_bounds__(512, 2 * ws_blocks_per_cu(COUT, CIB)) void k_halo_w
 
     if (is_loader) {
         // =========================================================== loader waves
-        if (WS_PRIO) __builtin_amdgcn_s_setprio(WS_PRIO);
+        // not for the 128 dy x 32 x blocks: their loaders transform half the x halo per tile, and at equal priority the
+        // MFMA waves issue first (tools/conv_micro.py --wgrad-step, two rounds: 2-5 % faster at every such shape)
+        constexpr int prio = (COUT == 128 && !BNB) ? 0 : WS_PRIO;
+        if (prio) __builtin_amdgcn_s_setprio(prio);
         // item = ltid + 256 i -> (pixel item / P, 16-B piece ltid % P) for P pieces per pixel: the piece is
         // fixed per thread; an 8-lane ds_write_b128 group covers one pixel's 8 pieces at the 10-slot row
         // stride (64 channels: conflict-free) or two pixels' 4 at the 6-slot stride
